@@ -1,0 +1,133 @@
+"""Exact dense convex QP solver -- oracle only (test infrastructure).
+
+Stands in for CVXPY -> OSQP / ECOS (mpc_controller.py:273-283, :471-480), which
+are not installed in this image.  Solves
+
+    min 1/2 w'Hw + c'w   s.t.  E w = f,  G w >= h
+
+with a Mehrotra predictor-corrector primal-dual interior point method on the
+dense KKT system, then "polishes" the result by identifying the active set
+(z_i > t_i) and solving the equality-constrained KKT system exactly, keeping the
+polished point only if it is primal and dual feasible.  The polished solution
+is exact to rounding, which is what OSQP's own polish step returns when it
+identifies the active set (189/200 logged solves agree to 1e-9).
+
+This algorithm is deliberately different from the product kernel (which
+condenses the horizon, eliminates the slacks and runs a Riccati-based active
+set method), so oracle and product cannot share a bug.
+"""
+import numpy as np
+
+
+class QPResult:
+    __slots__ = ("w", "status", "iters", "polished", "z", "y")
+
+    def __init__(self, w, status, iters, polished, z=None, y=None):
+        self.w = w
+        self.status = status
+        self.iters = iters
+        self.polished = polished
+        self.z = z
+        self.y = y
+
+
+def _kkt_solve(M, E, r1, r2):
+    n = M.shape[0]
+    m = E.shape[0]
+    K = np.zeros((n + m, n + m))
+    K[:n, :n] = M
+    K[:n, n:] = E.T
+    K[n:, :n] = E
+    rhs = np.concatenate([r1, r2])
+    try:
+        sol = np.linalg.solve(K, rhs)
+        if not np.all(np.isfinite(sol)):
+            raise np.linalg.LinAlgError
+    except np.linalg.LinAlgError:
+        sol = np.linalg.lstsq(K, rhs, rcond=None)[0]
+    return sol[:n], sol[n:]
+
+
+def solve_qp(H, c, E, f, G, h, max_iter=100, tol=1e-11, polish=True):
+    n = H.shape[0]
+    m = E.shape[0]
+    p = G.shape[0]
+    w = np.zeros(n)
+    y = np.zeros(m)
+    if p:
+        t = np.maximum(G @ w - h, 1.0)
+        z = np.ones(p)
+    else:
+        t = np.zeros(0)
+        z = np.zeros(0)
+    scale = 1.0 + max(np.abs(c).max(initial=0), np.abs(h).max(initial=0),
+                      np.abs(f).max(initial=0))
+    status = "max_iter"
+    it = 0
+    for it in range(1, max_iter + 1):
+        rd = H @ w + c - E.T @ y - G.T @ z
+        re = E @ w - f
+        ri = G @ w - t - h
+        mu = (t @ z) / p if p else 0.0
+        if (max(np.abs(rd).max(initial=0), np.abs(re).max(initial=0),
+                np.abs(ri).max(initial=0)) < tol * scale and mu < tol * scale):
+            status = "optimal"
+            break
+        D = z / t if p else np.zeros(0)
+        M = H + (G.T * D) @ G
+
+        def direction(rc):
+            r1 = -rd + G.T @ ((rc - z * ri) / t) if p else -rd
+            dw, ndy = _kkt_solve(M, E, r1, -re)
+            dt = G @ dw + ri
+            dz = (rc - z * dt) / t if p else np.zeros(0)
+            return dw, -ndy, dt, dz
+
+        # predictor
+        dw, dy, dt, dz = direction(-t * z)
+
+        def step(v, dv):
+            neg = dv < 0
+            if not np.any(neg):
+                return 1.0
+            return min(1.0, float(np.min(-v[neg] / dv[neg])))
+
+        if p:
+            ap = step(t, dt)
+            ad = step(z, dz)
+            mu_aff = ((t + ap * dt) @ (z + ad * dz)) / p
+            sigma = (mu_aff / mu) ** 3 if mu > 0 else 0.0
+            dw, dy, dt, dz = direction(-t * z + sigma * mu - dt * dz)
+            ap = 0.995 * step(t, dt)
+            ad = 0.995 * step(z, dz)
+            a = min(ap, ad)
+        else:
+            a = 1.0
+        w = w + a * dw
+        y = y + a * dy
+        if p:
+            t = t + a * dt
+            z = z + a * dz
+            t = np.maximum(t, 1e-300)
+            z = np.maximum(z, 1e-300)
+    res = QPResult(w, status, it, False, z, y)
+    if not polish:
+        return res
+    # ---- active-set polish --------------------------------------------------
+    act = z > t if p else np.zeros(0, dtype=bool)
+    GA = G[act]
+    hA = h[act]
+    C = np.vstack([E, GA])
+    d = np.concatenate([f, hA])
+    wp, lam = _kkt_solve(H, C, -c, d)
+    lam = -lam
+    ok = np.all(np.isfinite(wp))
+    if ok and p:
+        slack = G @ wp - h
+        ok = (np.all(slack[~act] >= -1e-9 * (1 + np.abs(h[~act])))
+              and np.all(lam[m:] >= -1e-9 * scale))
+    if ok and (status == "optimal" or np.abs(wp - w).max() < 1e-6 * (1 + np.abs(w).max())):
+        res.w = wp
+        res.polished = True
+        res.status = "optimal"
+    return res
