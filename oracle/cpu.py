@@ -1,0 +1,115 @@
+"""ctypes wrapper of oracle/c/librmpc_cpu.so -- the C restatement used as the timed CPU
+baseline ("port") by bench.py and as a second check in tests (test infrastructure only).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+class MpcParams(C.Structure):
+    """Mirror of RmpcMpcParams (include/rmpc.h)."""
+    _fields_ = [("horizon", C.c_int32), ("block_size", C.c_int32), ("formulation", C.c_int32),
+                ("soft", C.c_int32), ("precision", C.c_int32), ("max_iter", C.c_int32),
+                ("ramp_up_steps", C.c_int32), ("_pad0", C.c_int32), ("Q", C.c_double * 3),
+                ("R", C.c_double * 2), ("P", C.c_double * 3), ("d_safe", C.c_double),
+                ("slack_penalty", C.c_double), ("v_max", C.c_double),
+                ("omega_max", C.c_double), ("dt", C.c_double)]
+
+
+class LqrParams(C.Structure):
+    _fields_ = [("Q", C.c_double * 3), ("R", C.c_double * 2), ("dt", C.c_double),
+                ("v_max", C.c_double), ("omega_max", C.c_double), ("max_iter", C.c_int32),
+                ("use_cache", C.c_int32)]
+
+
+class LqrCache(C.Structure):
+    _fields_ = [("K", C.c_double * 6), ("last_v", C.c_double), ("last_theta", C.c_double),
+                ("valid", C.c_int32), ("_pad0", C.c_int32)]
+
+
+def build():
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(_HERE, "c")], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "c", "librmpc_cpu.so")
+        if not os.path.exists(path):
+            build()
+        _LIB = C.CDLL(path)
+    return _LIB
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def mpc_params(N, Q, R, P, d_safe, rho, v_max, omega_max, dt, block_size=1, ltv=True,
+               soft=True, max_iter=64, ramp=10):
+    p = MpcParams()
+    p.horizon, p.block_size, p.formulation, p.soft = N, block_size, 0 if ltv else 1, int(soft)
+    p.precision, p.max_iter, p.ramp_up_steps = 0, max_iter, ramp
+    p.Q[:] = list(Q)
+    p.R[:] = list(R)
+    p.P[:] = list(P)
+    p.d_safe, p.slack_penalty, p.v_max, p.omega_max, p.dt = d_safe, rho, v_max, omega_max, dt
+    return p
+
+
+def mpc_solve_batch(p, x0, x_refs, u_refs, obstacles, step_count=None, threads=1):
+    x0 = np.ascontiguousarray(x0, dtype=np.float64)
+    x_refs = np.ascontiguousarray(x_refs, dtype=np.float64)
+    u_refs = np.ascontiguousarray(u_refs, dtype=np.float64)
+    obs = np.ascontiguousarray(np.asarray(obstacles, dtype=np.float64).reshape(-1, 3))
+    B, N = x0.shape[0], p.horizon
+    out = dict(u0=np.zeros((B, 2)), u_seq=np.zeros((B, N, 2)), x_pred=np.zeros((B, N + 1, 3)),
+               cost=np.zeros(B), status=np.zeros(B, np.int32), slack_used=np.zeros(B, np.uint8),
+               iters=np.zeros(B, np.int32))
+    f = lib().rmpc_cpu_mpc_solve_batch
+    f.restype = C.c_int
+    rc = f(C.byref(p), C.c_int64(B), _p(x0), _p(x_refs), C.c_int32(x_refs.shape[1]), _p(u_refs),
+           C.c_int32(u_refs.shape[1]), _p(obs), C.c_int32(obs.shape[0]), _p(step_count),
+           _p(out["u0"]), _p(out["u_seq"]), _p(out["x_pred"]), _p(out["cost"]),
+           _p(out["status"]), _p(out["slack_used"]), _p(out["iters"]), C.c_int32(threads))
+    if rc != 0:
+        raise ValueError(f"rmpc_cpu_mpc_solve_batch -> {rc}")
+    return out
+
+
+def lqr_params(Q, R, dt, v_max, omega_max, max_iter=64, use_cache=1):
+    p = LqrParams()
+    p.Q[:] = list(Q)
+    p.R[:] = list(R)
+    p.dt, p.v_max, p.omega_max, p.max_iter, p.use_cache = dt, v_max, omega_max, max_iter, use_cache
+    return p
+
+
+def lqr_gain_batch(p, v_r, theta_r, guard=1, threads=1):
+    v_r = np.ascontiguousarray(v_r, dtype=np.float64)
+    theta_r = np.ascontiguousarray(theta_r, dtype=np.float64)
+    B = v_r.shape[0]
+    K = np.zeros((B, 2, 3))
+    P = np.zeros((B, 3, 3))
+    st = np.zeros(B, np.int32)
+    lib().rmpc_cpu_lqr_gain_batch(C.byref(p), C.c_int64(B), _p(v_r), _p(theta_r),
+                                  C.c_int32(guard), _p(K), _p(P), _p(st), C.c_int32(threads))
+    return K, P, st
+
+
+def lqr_control_batch(p, x, x_ref, u_ref, cache=None, threads=1):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    x_ref = np.ascontiguousarray(x_ref, dtype=np.float64)
+    u_ref = np.ascontiguousarray(u_ref, dtype=np.float64)
+    B = x.shape[0]
+    u = np.zeros((B, 2))
+    e = np.zeros((B, 3))
+    lib().rmpc_cpu_lqr_control_batch(C.byref(p), C.c_int64(B), _p(x), _p(x_ref), _p(u_ref),
+                                     None if cache is None else cache, _p(u), _p(e),
+                                     C.c_int32(threads))
+    return u, e

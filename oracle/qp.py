@@ -64,15 +64,19 @@ def solve_qp(H, c, E, f, G, h, max_iter=100, tol=1e-11, polish=True):
                       np.abs(f).max(initial=0))
     status = "max_iter"
     it = 0
+    res0 = mu0 = None
     for it in range(1, max_iter + 1):
         rd = H @ w + c - E.T @ y - G.T @ z
         re = E @ w - f
         ri = G @ w - t - h
         mu = (t @ z) / p if p else 0.0
-        if (max(np.abs(rd).max(initial=0), np.abs(re).max(initial=0),
-                np.abs(ri).max(initial=0)) < tol * scale and mu < tol * scale):
+        resn = max(np.abs(rd).max(initial=0), np.abs(re).max(initial=0),
+                   np.abs(ri).max(initial=0))
+        if resn < tol * scale and mu < tol * scale:
             status = "optimal"
             break
+        if res0 is None:
+            res0, mu0 = max(resn, 1e-300), max(mu, 1e-300)
         D = z / t if p else np.zeros(0)
         M = H + (G.T * D) @ G
 
@@ -97,6 +101,10 @@ def solve_qp(H, c, E, f, G, h, max_iter=100, tol=1e-11, polish=True):
             ad = step(z, dz)
             mu_aff = ((t + ap * dt) @ (z + ad * dz)) / p
             sigma = (mu_aff / mu) ** 3 if mu > 0 else 0.0
+            # safeguard: do not let complementarity outrun infeasibility (keeps the
+            # iterates centred; plain Mehrotra stalls on some slack-heavy instances)
+            if resn / res0 > 10.0 * mu / mu0:
+                sigma = max(sigma, 0.5)
             dw, dy, dt, dz = direction(-t * z + sigma * mu - dt * dz)
             ap = 0.995 * step(t, dt)
             ad = 0.995 * step(z, dz)
@@ -114,20 +122,32 @@ def solve_qp(H, c, E, f, G, h, max_iter=100, tol=1e-11, polish=True):
     if not polish:
         return res
     # ---- active-set polish --------------------------------------------------
+    # Start from the interior-point active set (z_i > t_i) and refine it by
+    # primal-dual active-set exchanges on the full KKT system until the polished
+    # point is primal feasible with nonnegative multipliers (exact to rounding).
     act = z > t if p else np.zeros(0, dtype=bool)
-    GA = G[act]
-    hA = h[act]
-    C = np.vstack([E, GA])
-    d = np.concatenate([f, hA])
-    wp, lam = _kkt_solve(H, C, -c, d)
-    lam = -lam
-    ok = np.all(np.isfinite(wp))
-    if ok and p:
+    seen = set()
+    for _ in range(50):
+        key = act.tobytes()
+        if key in seen:
+            break
+        seen.add(key)
+        C = np.vstack([E, G[act]])
+        d = np.concatenate([f, h[act]])
+        wp, lam = _kkt_solve(H, C, -c, d)
+        lam = -lam
+        if not np.all(np.isfinite(wp)):
+            break
+        if not p:
+            res.w, res.polished, res.status = wp, True, "optimal"
+            break
         slack = G @ wp - h
-        ok = (np.all(slack[~act] >= -1e-9 * (1 + np.abs(h[~act])))
-              and np.all(lam[m:] >= -1e-9 * scale))
-    if ok and (status == "optimal" or np.abs(wp - w).max() < 1e-6 * (1 + np.abs(w).max())):
-        res.w = wp
-        res.polished = True
-        res.status = "optimal"
+        viol = (~act) & (slack < -1e-10 * (1 + np.abs(h)))
+        lz = np.zeros(p)
+        lz[act] = lam[m:]
+        neg = act & (lz < -1e-10 * scale)
+        if not viol.any() and not neg.any():
+            res.w, res.polished, res.status = wp, True, "optimal"
+            break
+        act = (act | viol) & ~neg
     return res

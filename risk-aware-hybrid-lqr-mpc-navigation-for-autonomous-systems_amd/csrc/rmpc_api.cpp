@@ -1,0 +1,528 @@
+// rmpc_api.cpp -- the C-ABI of librmpc.so (see include/rmpc.h).
+//
+// Host-pointer entry points stage through device buffers owned by the context (grow-only,
+// allocated outside the launch path) on the context's stream and return after the
+// results are back; the _dev entry points only validate and enqueue on the caller's
+// stream.  There is no CPU compute path: every result is produced by a HIP kernel.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/rmpc.h"
+#include "rmpc_internal.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail(RMPC_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));          \
+    } while (0)
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) {
+            hipError_t e = hipFree(p);
+            if (e != hipSuccess) return e;
+        }
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes + bytes / 4 + 256;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+}  // namespace
+
+enum {
+    SB_X0, SB_XREF, SB_UREF, SB_OBS, SB_STEP, SB_U0, SB_USEQ, SB_XPRED, SB_COST, SB_STATUS,
+    SB_SLACK, SB_ITERS, SB_CACHE, SB_ERR, SB_K, SB_P, SB_EXTRA0, SB_EXTRA1, SB_EXTRA2, SB_EXTRA3,
+    SB_COUNT
+};
+
+struct RmpcCtx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevBuf ws;                 // solver workspace
+    DevBuf stage[SB_COUNT];    // staging buffers for host-pointer entry points
+    DevBuf idx_lqr, idx_mpc, counts, hyb_status;
+    std::mutex mu;
+};
+
+static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+extern "C" {
+
+int rmpc_abi_version(void) { return RMPC_ABI_VERSION; }
+
+const char *rmpc_last_error(void) { return g_last_error.c_str(); }
+
+int rmpc_device_count(int *count) {
+    if (!count) return fail(RMPC_EINVAL, "count is NULL");
+    HIP_TRY(hipGetDeviceCount(count));
+    return RMPC_OK;
+}
+
+int rmpc_ctx_create(int device_id, RmpcCtx **out) {
+    if (!out) return fail(RMPC_EINVAL, "out is NULL");
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (device_id < 0 || device_id >= n) return fail(RMPC_EINVAL, "device %d out of range (%d devices)", device_id, n);
+    HIP_TRY(hipSetDevice(device_id));
+    RmpcCtx *c = new RmpcCtx();
+    c->device = device_id;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return fail(RMPC_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    *out = c;
+    return RMPC_OK;
+}
+
+int rmpc_ctx_destroy(RmpcCtx *c) {
+    if (!c) return RMPC_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    c->ws.release();
+    for (auto &b : c->stage) b.release();
+    c->idx_lqr.release();
+    c->idx_mpc.release();
+    c->counts.release();
+    c->hyb_status.release();
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return RMPC_OK;
+}
+
+int rmpc_ctx_synchronize(RmpcCtx *c) {
+    if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RMPC_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------ helpers
+static int check_mpc_params(const RmpcMpcParams *p, int ref_rows, int uref_rows, int n_obs) {
+    if (!p) return fail(RMPC_EINVAL, "params is NULL");
+    const int N = p->horizon;
+    if (N < 1 || N > RMPC_MAX_HORIZON) return fail(RMPC_EINVAL, "horizon %d not in [1, %d]", N, RMPC_MAX_HORIZON);
+    if (n_obs < 0 || n_obs > RMPC_MAX_OBSTACLES) return fail(RMPC_EINVAL, "n_obs %d not in [0, %d]", n_obs, RMPC_MAX_OBSTACLES);
+    if (p->formulation != RMPC_LTV && p->formulation != RMPC_LTI) return fail(RMPC_EINVAL, "bad formulation %d", p->formulation);
+    if (p->formulation == RMPC_LTV) {
+        if (p->block_size < 1) return fail(RMPC_EINVAL, "block_size %d < 1", p->block_size);
+        if (ref_rows < N + 1) return fail(RMPC_EINVAL, "LTV needs ref_rows >= N+1 (%d < %d)", ref_rows, N + 1);
+        if (uref_rows < N) return fail(RMPC_EINVAL, "LTV needs uref_rows >= N (%d < %d)", uref_rows, N);
+    }
+    if (ref_rows < 1 || uref_rows < 1) return fail(RMPC_EINVAL, "empty reference arrays");
+    if (!p->soft && n_obs > 0)
+        return fail(RMPC_ENOTSUP, "use_soft_constraints=False with obstacles (hard half-spaces) is not supported yet");
+    if (p->precision != RMPC_F64) return fail(RMPC_ENOTSUP, "precision %d not supported yet", p->precision);
+    if (!(p->dt > 0) || !(p->slack_penalty >= 0) || !(p->R[0] > 0) || !(p->R[1] > 0))
+        return fail(RMPC_EINVAL, "dt, R must be > 0 and slack_penalty >= 0");
+    return RMPC_OK;
+}
+
+static MpcDevParams to_dev(const RmpcMpcParams *p) {
+    MpcDevParams d;
+    for (int i = 0; i < 3; i++) { d.Q[i] = p->Q[i]; d.P[i] = p->P[i]; }
+    d.R[0] = p->R[0];
+    d.R[1] = p->R[1];
+    d.d_safe = p->d_safe;
+    d.rho = p->slack_penalty;
+    d.v_max = p->v_max;
+    d.omega_max = p->omega_max;
+    d.dt = p->dt;
+    d.ltv = p->formulation == RMPC_LTV;
+    d.soft = p->soft;
+    d.max_iter = p->max_iter > 0 ? p->max_iter : 64;
+    d.ramp_up_steps = p->ramp_up_steps > 0 ? p->ramp_up_steps : 10;
+    return d;
+}
+
+static LqrDevParams to_dev(const RmpcLqrParams *p) {
+    LqrDevParams d;
+    for (int i = 0; i < 3; i++) d.Q[i] = p->Q[i];
+    d.R[0] = p->R[0];
+    d.R[1] = p->R[1];
+    d.dt = p->dt;
+    d.v_max = p->v_max;
+    d.omega_max = p->omega_max;
+    d.max_iter = p->max_iter > 0 ? p->max_iter : 64;
+    d.use_cache = p->use_cache;
+    return d;
+}
+
+static RiskDevParams to_dev(const RmpcRiskParams *p) {
+    RiskDevParams d;
+    d.d_safe = p->d_safe;
+    d.d_trigger = p->d_trigger;
+    d.alpha = p->alpha;
+    d.beta = p->beta;
+    d.th_low = p->threshold_low;
+    d.th_med = p->threshold_medium;
+    d.th_high = p->threshold_high;
+    d.min_dwell = p->min_dwell_steps;
+    return d;
+}
+
+static hipError_t ensure_ws(RmpcCtx *c, const MpcLayout &L, int64_t B) {
+    const size_t waves = (size_t)((B + RMPC_WAVE_LANES - 1) / RMPC_WAVE_LANES);
+    return c->ws.ensure(waves * (size_t)L.REC * RMPC_WAVE_LANES * sizeof(double));
+}
+
+static hipStream_t pick(RmpcCtx *c, void *s) { return s ? (hipStream_t)s : c->stream; }
+
+// stage a host array to the device (returns device pointer or nullptr when src is null)
+template <typename T>
+static int h2d(RmpcCtx *c, int slot, const T *src, size_t n, T **dst) {
+    if (!src) { *dst = nullptr; return RMPC_OK; }
+    HIP_TRY(c->stage[slot].ensure(align_up(n * sizeof(T), 256)));
+    HIP_TRY(hipMemcpyAsync(c->stage[slot].p, src, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+    *dst = (T *)c->stage[slot].p;
+    return RMPC_OK;
+}
+
+template <typename T>
+static int dalloc(RmpcCtx *c, int slot, const T *host, size_t n, T **dst) {
+    if (!host) { *dst = nullptr; return RMPC_OK; }
+    HIP_TRY(c->stage[slot].ensure(align_up(n * sizeof(T), 256)));
+    *dst = (T *)c->stage[slot].p;
+    return RMPC_OK;
+}
+
+template <typename T>
+static int d2h(RmpcCtx *c, T *host, const T *dev, size_t n) {
+    if (!host) return RMPC_OK;
+    HIP_TRY(hipMemcpyAsync(host, dev, n * sizeof(T), hipMemcpyDeviceToHost, c->stream));
+    return RMPC_OK;
+}
+
+#define RC(x)                           \
+    do {                                \
+        int rc_ = (x);                  \
+        if (rc_ != RMPC_OK) return rc_; \
+    } while (0)
+
+// ------------------------------------------------------------------------------ MPC
+extern "C" int rmpc_mpc_solve_batch_dev(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const double *x0,
+                                        const double *x_refs, int32_t ref_rows, const double *u_refs,
+                                        int32_t uref_rows, const double *obstacles, int32_t n_obs,
+                                        int32_t *step_count, double *u0, double *u_seq, double *x_pred,
+                                        double *cost, int32_t *status, uint8_t *slack_used, int32_t *iters,
+                                        void *stream) {
+    if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
+    RC(check_mpc_params(p, ref_rows, uref_rows, n_obs));
+    if (B < 0) return fail(RMPC_EINVAL, "B < 0");
+    if (B == 0) return RMPC_OK;
+    if (!x0 || !x_refs || !u_refs || !u0 || !status || (n_obs > 0 && !obstacles))
+        return fail(RMPC_EINVAL, "required pointer is NULL");
+    HIP_TRY(hipSetDevice(c->device));
+    const int bs = p->formulation == RMPC_LTV ? p->block_size : 1;
+    const MpcLayout L = rmpc_mpc_layout(p->horizon, bs, n_obs);
+    HIP_TRY(ensure_ws(c, L, B));
+    const MpcDevParams d = to_dev(p);
+    HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
+                                step_count, u0, u_seq, x_pred, cost, status, slack_used, iters, c->ws.p,
+                                nullptr, nullptr, pick(c, stream)));
+    return RMPC_OK;
+}
+
+extern "C" int rmpc_mpc_solve_batch(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const double *x0,
+                                    const double *x_refs, int32_t ref_rows, const double *u_refs,
+                                    int32_t uref_rows, const double *obstacles, int32_t n_obs,
+                                    int32_t *step_count, double *u0, double *u_seq, double *x_pred,
+                                    double *cost, int32_t *status, uint8_t *slack_used, int32_t *iters) {
+    if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
+    RC(check_mpc_params(p, ref_rows, uref_rows, n_obs));
+    if (B < 0) return fail(RMPC_EINVAL, "B < 0");
+    if (B == 0) return RMPC_OK;
+    if (!x0 || !x_refs || !u_refs || !u0 || !status || (n_obs > 0 && !obstacles))
+        return fail(RMPC_EINVAL, "required pointer is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    const int N = p->horizon;
+    double *dx0, *dxr, *dur, *dobs = nullptr, *du0, *duseq, *dxp, *dcost;
+    int32_t *dstep, *dst, *dit;
+    uint8_t *dsl;
+    RC(h2d(c, SB_X0, x0, (size_t)B * 3, &dx0));
+    RC(h2d(c, SB_XREF, x_refs, (size_t)B * ref_rows * 3, &dxr));
+    RC(h2d(c, SB_UREF, u_refs, (size_t)B * uref_rows * 2, &dur));
+    if (n_obs > 0) RC(h2d(c, SB_OBS, obstacles, (size_t)n_obs * 3, &dobs));
+    RC(h2d(c, SB_STEP, step_count, (size_t)B, &dstep));
+    RC(dalloc(c, SB_U0, u0, (size_t)B * 2, &du0));
+    RC(dalloc(c, SB_USEQ, u_seq, (size_t)B * N * 2, &duseq));
+    RC(dalloc(c, SB_XPRED, x_pred, (size_t)B * (N + 1) * 3, &dxp));
+    RC(dalloc(c, SB_COST, cost, (size_t)B, &dcost));
+    RC(dalloc(c, SB_STATUS, status, (size_t)B, &dst));
+    RC(dalloc(c, SB_SLACK, slack_used, (size_t)B, &dsl));
+    RC(dalloc(c, SB_ITERS, iters, (size_t)B, &dit));
+    RC(rmpc_mpc_solve_batch_dev(c, p, B, dx0, dxr, ref_rows, dur, uref_rows, dobs, n_obs, dstep, du0,
+                                duseq, dxp, dcost, dst, dsl, dit, c->stream));
+    RC(d2h(c, u0, du0, (size_t)B * 2));
+    RC(d2h(c, u_seq, duseq, (size_t)B * N * 2));
+    RC(d2h(c, x_pred, dxp, (size_t)B * (N + 1) * 3));
+    RC(d2h(c, cost, dcost, (size_t)B));
+    RC(d2h(c, status, dst, (size_t)B));
+    RC(d2h(c, slack_used, dsl, (size_t)B));
+    RC(d2h(c, iters, dit, (size_t)B));
+    RC(d2h(c, step_count, dstep, (size_t)B));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RMPC_OK;
+}
+
+// ------------------------------------------------------------------------------ LQR
+static int check_lqr(const RmpcLqrParams *p) {
+    if (!p) return fail(RMPC_EINVAL, "params is NULL");
+    if (!(p->dt > 0) || !(p->R[0] > 0) || !(p->R[1] > 0)) return fail(RMPC_EINVAL, "dt, R must be > 0");
+    return RMPC_OK;
+}
+
+extern "C" int rmpc_lqr_control_batch_dev(RmpcCtx *c, const RmpcLqrParams *p, int64_t B, const double *x,
+                                          const double *x_ref, const double *u_ref, RmpcLqrCache *cache,
+                                          double *u_out, double *err_out, double *K_out, double *P_out,
+                                          int32_t *status, void *stream) {
+    if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
+    RC(check_lqr(p));
+    if (B < 0) return fail(RMPC_EINVAL, "B < 0");
+    if (B == 0) return RMPC_OK;
+    if (!x || !x_ref || !u_ref || !u_out) return fail(RMPC_EINVAL, "required pointer is NULL");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(rmpc_launch_lqr_control(to_dev(p), B, x, x_ref, 3, u_ref, 2, cache, u_out, err_out, K_out,
+                                    P_out, status, nullptr, nullptr, pick(c, stream)));
+    return RMPC_OK;
+}
+
+extern "C" int rmpc_lqr_control_batch(RmpcCtx *c, const RmpcLqrParams *p, int64_t B, const double *x,
+                                      const double *x_ref, const double *u_ref, RmpcLqrCache *cache,
+                                      double *u_out, double *err_out, double *K_out, double *P_out,
+                                      int32_t *status) {
+    if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
+    RC(check_lqr(p));
+    if (B < 0) return fail(RMPC_EINVAL, "B < 0");
+    if (B == 0) return RMPC_OK;
+    if (!x || !x_ref || !u_ref || !u_out) return fail(RMPC_EINVAL, "required pointer is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    double *dx, *dxr, *dur, *du, *de, *dK, *dP;
+    int32_t *dst;
+    RmpcLqrCache *dc;
+    RC(h2d(c, SB_X0, x, (size_t)B * 3, &dx));
+    RC(h2d(c, SB_XREF, x_ref, (size_t)B * 3, &dxr));
+    RC(h2d(c, SB_UREF, u_ref, (size_t)B * 2, &dur));
+    RC(h2d(c, SB_CACHE, cache, (size_t)B, &dc));
+    RC(dalloc(c, SB_U0, u_out, (size_t)B * 2, &du));
+    RC(dalloc(c, SB_ERR, err_out, (size_t)B * 3, &de));
+    RC(dalloc(c, SB_K, K_out, (size_t)B * 6, &dK));
+    RC(dalloc(c, SB_P, P_out, (size_t)B * 9, &dP));
+    RC(dalloc(c, SB_STATUS, status, (size_t)B, &dst));
+    RC(rmpc_lqr_control_batch_dev(c, p, B, dx, dxr, dur, dc, du, de, dK, dP, dst, c->stream));
+    RC(d2h(c, u_out, du, (size_t)B * 2));
+    RC(d2h(c, err_out, de, (size_t)B * 3));
+    RC(d2h(c, K_out, dK, (size_t)B * 6));
+    RC(d2h(c, P_out, dP, (size_t)B * 9));
+    RC(d2h(c, status, dst, (size_t)B));
+    RC(d2h(c, cache, dc, (size_t)B));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RMPC_OK;
+}
+
+extern "C" int rmpc_lqr_gain_batch(RmpcCtx *c, const RmpcLqrParams *p, int64_t B, const double *v_r,
+                                   const double *theta_r, int32_t guard_v, double *K_out, double *P_out,
+                                   int32_t *status) {
+    if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
+    RC(check_lqr(p));
+    if (B < 0) return fail(RMPC_EINVAL, "B < 0");
+    if (B == 0) return RMPC_OK;
+    if (!v_r || !theta_r || !K_out) return fail(RMPC_EINVAL, "required pointer is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    double *dv, *dth, *dK, *dP;
+    int32_t *dst;
+    RC(h2d(c, SB_X0, v_r, (size_t)B, &dv));
+    RC(h2d(c, SB_XREF, theta_r, (size_t)B, &dth));
+    RC(dalloc(c, SB_K, K_out, (size_t)B * 6, &dK));
+    RC(dalloc(c, SB_P, P_out, (size_t)B * 9, &dP));
+    RC(dalloc(c, SB_STATUS, status, (size_t)B, &dst));
+    HIP_TRY(rmpc_launch_lqr_gain(to_dev(p), B, dv, dth, guard_v, dK, dP, dst, c->stream));
+    RC(d2h(c, K_out, dK, (size_t)B * 6));
+    RC(d2h(c, P_out, dP, (size_t)B * 9));
+    RC(d2h(c, status, dst, (size_t)B));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RMPC_OK;
+}
+
+// ------------------------------------------------------------------------------ risk / hybrid
+extern "C" int rmpc_risk_batch(RmpcCtx *c, const RmpcRiskParams *rp, int64_t B, const double *x,
+                               const double *pred, int32_t n_pred, const double *obstacles, int32_t n_obs,
+                               double *out, uint8_t *use_mpc, int32_t *level) {
+    if (!c || !rp) return fail(RMPC_EINVAL, "ctx/params is NULL");
+    if (B < 0 || n_obs < 0 || n_obs > RMPC_MAX_OBSTACLES || (pred && n_pred < 0)) return fail(RMPC_EINVAL, "bad shape");
+    if (B == 0) return RMPC_OK;
+    if (!x || !out || (n_obs > 0 && !obstacles)) return fail(RMPC_EINVAL, "required pointer is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    double *dx, *dp, *dobs = nullptr, *dout;
+    uint8_t *dm;
+    int32_t *dl;
+    RC(h2d(c, SB_X0, x, (size_t)B * 3, &dx));
+    RC(h2d(c, SB_XREF, pred, (size_t)B * (pred ? n_pred : 0) * 3, &dp));
+    if (n_obs > 0) RC(h2d(c, SB_OBS, obstacles, (size_t)n_obs * 3, &dobs));
+    RC(dalloc(c, SB_U0, out, (size_t)B * 5, &dout));
+    RC(dalloc(c, SB_SLACK, use_mpc, (size_t)B, &dm));
+    RC(dalloc(c, SB_STATUS, level, (size_t)B, &dl));
+    HIP_TRY(rmpc_launch_risk(to_dev(rp), B, dx, dp, n_pred, dobs, n_obs, dout, dm, dl, c->stream));
+    RC(d2h(c, out, dout, (size_t)B * 5));
+    RC(d2h(c, use_mpc, dm, (size_t)B));
+    RC(d2h(c, level, dl, (size_t)B));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RMPC_OK;
+}
+
+extern "C" int rmpc_hybrid_step_batch_dev(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams *lp,
+                                          const RmpcMpcParams *mp, int64_t B, const double *x,
+                                          const double *x_refs, int32_t ref_rows, const double *u_refs,
+                                          int32_t uref_rows, const double *obstacles, int32_t n_obs,
+                                          int32_t *prev_ctrl, int32_t *steps_since, int32_t *step_count,
+                                          RmpcLqrCache *cache, double *u_out, uint8_t *used_mpc,
+                                          double *risk_out, void *stream) {
+    if (!c || !rp || !lp) return fail(RMPC_EINVAL, "ctx/params is NULL");
+    RC(check_mpc_params(mp, ref_rows, uref_rows, n_obs));
+    RC(check_lqr(lp));
+    if (mp->formulation != RMPC_LTV) return fail(RMPC_EINVAL, "hybrid uses solve_with_ltv (formulation LTV)");
+    if (B < 0) return fail(RMPC_EINVAL, "B < 0");
+    if (B == 0) return RMPC_OK;
+    if (!x || !x_refs || !u_refs || !prev_ctrl || !steps_since || !u_out || !used_mpc || (n_obs > 0 && !obstacles))
+        return fail(RMPC_EINVAL, "required pointer is NULL");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = pick(c, stream);
+    HIP_TRY(c->idx_lqr.ensure((size_t)B * sizeof(int32_t)));
+    HIP_TRY(c->idx_mpc.ensure((size_t)B * sizeof(int32_t)));
+    HIP_TRY(c->counts.ensure(256));
+    HIP_TRY(c->hyb_status.ensure((size_t)B * sizeof(int32_t)));
+    const MpcLayout L = rmpc_mpc_layout(mp->horizon, mp->block_size, n_obs);
+    HIP_TRY(ensure_ws(c, L, B));
+    int32_t *cnt = (int32_t *)c->counts.p;
+    HIP_TRY(hipMemsetAsync(cnt, 0, 16, s));
+    HIP_TRY(rmpc_launch_hybrid_decide(to_dev(rp), B, x, obstacles, n_obs, prev_ctrl, steps_since, used_mpc,
+                                      risk_out, (int32_t *)c->idx_lqr.p, (int32_t *)c->idx_mpc.p, cnt, s));
+    // LQR branch: x_ref / u_ref = row 0 of the segment (get_reference_at_index(k))
+    HIP_TRY(rmpc_launch_lqr_control(to_dev(lp), B, x, x_refs, ref_rows * 3, u_refs, uref_rows * 2, cache,
+                                    u_out, nullptr, nullptr, nullptr, nullptr, (const int32_t *)c->idx_lqr.p,
+                                    cnt, s));
+    // MPC branch: solve_with_ltv on the segment; writes u0 straight into u_out
+    HIP_TRY(rmpc_launch_mpc_f64(to_dev(mp), L, B, x, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
+                                step_count, u_out, nullptr, nullptr, nullptr,
+                                (int32_t *)c->hyb_status.p, nullptr, nullptr, c->ws.p,
+                                (const int32_t *)c->idx_mpc.p, cnt + 1, s));
+    return RMPC_OK;
+}
+
+extern "C" int rmpc_hybrid_step_batch(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams *lp,
+                                      const RmpcMpcParams *mp, int64_t B, const double *x,
+                                      const double *x_refs, int32_t ref_rows, const double *u_refs,
+                                      int32_t uref_rows, const double *obstacles, int32_t n_obs,
+                                      int32_t *prev_ctrl, int32_t *steps_since, int32_t *step_count,
+                                      RmpcLqrCache *cache, double *u_out, uint8_t *used_mpc, double *risk_out) {
+    if (!c || !rp || !lp) return fail(RMPC_EINVAL, "ctx/params is NULL");
+    RC(check_mpc_params(mp, ref_rows, uref_rows, n_obs));
+    if (B < 0) return fail(RMPC_EINVAL, "B < 0");
+    if (B == 0) return RMPC_OK;
+    if (!x || !x_refs || !u_refs || !prev_ctrl || !steps_since || !u_out || !used_mpc || (n_obs > 0 && !obstacles))
+        return fail(RMPC_EINVAL, "required pointer is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    double *dx, *dxr, *dur, *dobs = nullptr, *du, *drisk;
+    int32_t *dprev, *dsince, *dstep;
+    RmpcLqrCache *dc;
+    uint8_t *dused;
+    RC(h2d(c, SB_X0, x, (size_t)B * 3, &dx));
+    RC(h2d(c, SB_XREF, x_refs, (size_t)B * ref_rows * 3, &dxr));
+    RC(h2d(c, SB_UREF, u_refs, (size_t)B * uref_rows * 2, &dur));
+    if (n_obs > 0) RC(h2d(c, SB_OBS, obstacles, (size_t)n_obs * 3, &dobs));
+    RC(h2d(c, SB_EXTRA1, prev_ctrl, (size_t)B, &dprev));
+    RC(h2d(c, SB_EXTRA2, steps_since, (size_t)B, &dsince));
+    RC(h2d(c, SB_STEP, step_count, (size_t)B, &dstep));
+    RC(h2d(c, SB_CACHE, cache, (size_t)B, &dc));
+    RC(dalloc(c, SB_U0, u_out, (size_t)B * 2, &du));
+    RC(dalloc(c, SB_SLACK, used_mpc, (size_t)B, &dused));
+    RC(dalloc(c, SB_COST, risk_out, (size_t)B, &drisk));
+    RC(rmpc_hybrid_step_batch_dev(c, rp, lp, mp, B, dx, dxr, ref_rows, dur, uref_rows, dobs, n_obs, dprev,
+                                  dsince, dstep, dc, du, dused, drisk, c->stream));
+    RC(d2h(c, u_out, du, (size_t)B * 2));
+    RC(d2h(c, used_mpc, dused, (size_t)B));
+    RC(d2h(c, risk_out, drisk, (size_t)B));
+    RC(d2h(c, prev_ctrl, dprev, (size_t)B));
+    RC(d2h(c, steps_since, dsince, (size_t)B));
+    RC(d2h(c, step_count, dstep, (size_t)B));
+    RC(d2h(c, cache, dc, (size_t)B));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RMPC_OK;
+}
+
+// ------------------------------------------------------------------------------ plant / refs
+extern "C" int rmpc_plant_step_batch(RmpcCtx *c, int64_t B, const double *x, const double *u, double dt,
+                                     double v_max, double omega_max, int32_t method, double *x_next) {
+    if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
+    if (B < 0 || (method != 0 && method != 1)) return fail(RMPC_EINVAL, "bad shape/method");
+    if (B == 0) return RMPC_OK;
+    if (!x || !u || !x_next) return fail(RMPC_EINVAL, "required pointer is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    double *dx, *du, *dn;
+    RC(h2d(c, SB_X0, x, (size_t)B * 3, &dx));
+    RC(h2d(c, SB_UREF, u, (size_t)B * 2, &du));
+    RC(dalloc(c, SB_U0, x_next, (size_t)B * 3, &dn));
+    HIP_TRY(rmpc_launch_plant(B, dx, du, dt, v_max, omega_max, method, dn, c->stream));
+    RC(d2h(c, x_next, dn, (size_t)B * 3));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RMPC_OK;
+}
+
+extern "C" int rmpc_figure8_batch(RmpcCtx *c, int64_t B, const double *t0, int32_t rows, double A,
+                                  double a, double dt, double *x_refs, double *u_refs) {
+    if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
+    if (B < 0 || rows < 1) return fail(RMPC_EINVAL, "bad shape");
+    if (B == 0) return RMPC_OK;
+    if (!t0 || !x_refs || !u_refs) return fail(RMPC_EINVAL, "required pointer is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    double *dt0, *dxr, *dur;
+    RC(h2d(c, SB_X0, t0, (size_t)B, &dt0));
+    RC(dalloc(c, SB_XREF, x_refs, (size_t)B * rows * 3, &dxr));
+    RC(dalloc(c, SB_UREF, u_refs, (size_t)B * rows * 2, &dur));
+    HIP_TRY(rmpc_launch_figure8(B, dt0, rows, A, a, dt, dxr, dur, c->stream));
+    RC(d2h(c, x_refs, dxr, (size_t)B * rows * 3));
+    RC(d2h(c, u_refs, dur, (size_t)B * rows * 2));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RMPC_OK;
+}

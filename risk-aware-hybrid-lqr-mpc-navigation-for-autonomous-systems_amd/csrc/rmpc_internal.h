@@ -1,0 +1,70 @@
+// rmpc_internal.h -- host/device shared structs of librmpc.so (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rmpc.h"
+
+#define RMPC_PDAS_ITERS 8
+#define RMPC_WAVE_LANES 64
+
+// Flattened, kernel-argument form of RmpcMpcParams.
+struct MpcDevParams {
+    double Q[3], R[2], P[3];
+    double d_safe, rho, v_max, omega_max, dt;
+    int ltv, soft, max_iter, ramp_up_steps;
+};
+
+// Offsets (in elements) of the fields of one robot's workspace record.
+struct MpcLayout {
+    int N, bs, nb, no;
+    int A0, A1, B0, B1, US0, US1, XS0, XS1, XS2;
+    int LO0, LO1, HI0, HI1, BF0, BF1;
+    int HN0, HN1, HB, HACT;
+    int K;     // 8 * nb: K rows (6) + k (2), per block
+    int X0, X1, X2, U0, U1, Z0, Z1, G0, G1;
+    int REC;
+};
+
+MpcLayout rmpc_mpc_layout(int N, int bs, int no);
+
+hipError_t rmpc_launch_mpc_f64(const MpcDevParams &prm, const MpcLayout &L, int64_t B,
+                               const double *x0, const double *x_refs, int ref_rows,
+                               const double *u_refs, int uref_rows, const double *obstacles,
+                               int n_obs, int32_t *step_count, double *u0, double *u_seq,
+                               double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
+                               int32_t *iters, void *ws, const int32_t *index,
+                               const int32_t *count, hipStream_t stream);
+
+struct LqrDevParams {
+    double Q[3], R[2];
+    double dt, v_max, omega_max;
+    int max_iter, use_cache;
+};
+
+hipError_t rmpc_launch_lqr_control(const LqrDevParams &p, int64_t B, const double *x,
+                                   const double *x_ref, int xref_stride, const double *u_ref,
+                                   int uref_stride, RmpcLqrCache *cache, double *u_out,
+                                   double *err_out, double *K_out, double *P_out, int32_t *status,
+                                   const int32_t *index, const int32_t *count, hipStream_t stream);
+hipError_t rmpc_launch_lqr_gain(const LqrDevParams &p, int64_t B, const double *v_r,
+                                const double *theta_r, int guard, double *K_out, double *P_out,
+                                int32_t *status, hipStream_t stream);
+
+struct RiskDevParams {
+    double d_safe, d_trigger, alpha, beta, th_low, th_med, th_high;
+    int min_dwell;
+};
+
+hipError_t rmpc_launch_risk(const RiskDevParams &p, int64_t B, const double *x, const double *pred,
+                            int n_pred, const double *obstacles, int n_obs, double *out,
+                            uint8_t *use_mpc, int32_t *level, hipStream_t stream);
+hipError_t rmpc_launch_hybrid_decide(const RiskDevParams &p, int64_t B, const double *x,
+                                     const double *obstacles, int n_obs, int32_t *prev_ctrl,
+                                     int32_t *steps_since, uint8_t *used_mpc, double *risk_out,
+                                     int32_t *idx_lqr, int32_t *idx_mpc, int32_t *counts,
+                                     hipStream_t stream);
+hipError_t rmpc_launch_plant(int64_t B, const double *x, const double *u, double dt, double v_max,
+                             double omega_max, int method, double *x_next, hipStream_t stream);
+hipError_t rmpc_launch_figure8(int64_t B, const double *t0, int rows, double A, double a,
+                               double dt, double *x_refs, double *u_refs, hipStream_t stream);

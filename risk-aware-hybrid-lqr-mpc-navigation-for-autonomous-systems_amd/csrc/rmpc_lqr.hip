@@ -1,0 +1,247 @@
+// rmpc_lqr.hip -- batched LQR gain + control on CDNA4 (gfx950).
+//
+// Replaces LQRController.compute_control_at_operating_point (lqr_controller.py:191-215),
+// i.e. compute_gain (92-147: linearise at (v_r, theta_r), |v_r| < 1e-6 -> 0.01 guard,
+// DARE, K = (R + B'PB)^-1 B'PA, fallback K on failure, 1e-6 operating-point cache) and
+// compute_control (149-189: wrapped error, u = clip(u_ref - K e)).
+//
+// One lane per robot; the 3x3 DARE is solved in registers with the structure-preserving
+// doubling algorithm (SDA): A_{k+1} = A_k W^-1 A_k, G_{k+1} = G_k + A_k W^-1 G_k A_k',
+// H_{k+1} = H_k + A_k' H_k W^-1 A_k, W = I + G_k H_k, H_k -> P quadratically
+// (10-17 doubling steps on the Figure-8 operating range versus 350-42000 plain Riccati
+// fixed-point steps).  SciPy's solve_discrete_are (QZ) is the reference's
+// arithmetic; both return the unique stabilising solution.
+#include "rmpc_device.h"
+#include "rmpc_internal.h"
+
+namespace rmpc {
+
+struct M3 {
+    double m[3][3];
+};
+
+__device__ __forceinline__ M3 mul3(const M3 &A, const M3 &B) {
+    M3 C;
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) C.m[i][j] = A.m[i][0] * B.m[0][j] + A.m[i][1] * B.m[1][j] + A.m[i][2] * B.m[2][j];
+    return C;
+}
+
+__device__ __forceinline__ bool inv3(const M3 &M, M3 &I) {
+    const double c00 = M.m[1][1] * M.m[2][2] - M.m[1][2] * M.m[2][1];
+    const double c01 = M.m[1][2] * M.m[2][0] - M.m[1][0] * M.m[2][2];
+    const double c02 = M.m[1][0] * M.m[2][1] - M.m[1][1] * M.m[2][0];
+    const double det = M.m[0][0] * c00 + M.m[0][1] * c01 + M.m[0][2] * c02;
+    if (!(fabs(det) > 0.0) || !isfinite(det)) return false;
+    const double id = 1.0 / det;
+    I.m[0][0] = c00 * id;
+    I.m[1][0] = c01 * id;
+    I.m[2][0] = c02 * id;
+    I.m[0][1] = (M.m[0][2] * M.m[2][1] - M.m[0][1] * M.m[2][2]) * id;
+    I.m[1][1] = (M.m[0][0] * M.m[2][2] - M.m[0][2] * M.m[2][0]) * id;
+    I.m[2][1] = (M.m[0][1] * M.m[2][0] - M.m[0][0] * M.m[2][1]) * id;
+    I.m[0][2] = (M.m[0][1] * M.m[1][2] - M.m[0][2] * M.m[1][1]) * id;
+    I.m[1][2] = (M.m[0][2] * M.m[1][0] - M.m[0][0] * M.m[1][2]) * id;
+    I.m[2][2] = (M.m[0][0] * M.m[1][1] - M.m[0][1] * M.m[1][0]) * id;
+    return true;
+}
+
+// DARE + gain at one operating point; returns false when the DARE fails (fallback K).
+__device__ bool lqr_gain(const LqrDevParams &p, double v_r, double th, double K[6], M3 *Pout) {
+    double s, c;
+    sincos(th, &s, &c);
+    const double dt = p.dt;
+    M3 A = {{{1, 0, -v_r * s * dt}, {0, 1, v_r * c * dt}, {0, 0, 1}}};
+    const double B[3][2] = {{c * dt, 0}, {s * dt, 0}, {0, dt}};
+    M3 G, H = {{{p.Q[0], 0, 0}, {0, p.Q[1], 0}, {0, 0, p.Q[2]}}};
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) G.m[i][j] = B[i][0] * B[j][0] / p.R[0] + B[i][1] * B[j][1] / p.R[1];
+    M3 Ak = A;
+    bool conv = false, last = false;
+    for (int it = 0; it < p.max_iter; it++) {
+        M3 T = mul3(G, H), W, Wi;
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) W.m[i][j] = (i == j ? 1.0 : 0.0) + T.m[i][j];
+        if (!inv3(W, Wi)) return false;
+        const M3 WiA = mul3(Wi, Ak), WiG = mul3(Wi, G);
+        const M3 nA = mul3(Ak, WiA), AWG = mul3(Ak, WiG), HWA = mul3(H, WiA);
+        double dH = 0, nrm = 0;
+        M3 nG, nH;
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                double g = G.m[i][j], h = H.m[i][j];
+#pragma unroll
+                for (int l = 0; l < 3; l++) {
+                    g += AWG.m[i][l] * Ak.m[j][l];
+                    h += Ak.m[l][i] * HWA.m[l][j];
+                }
+                nG.m[i][j] = g;
+                nH.m[i][j] = h;
+            }
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                dH = fmax(dH, fabs(nH.m[i][j] - H.m[i][j]));
+                nrm = fmax(nrm, fabs(nH.m[i][j]));
+                Ak.m[i][j] = nA.m[i][j];
+            }
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                G.m[i][j] = 0.5 * (nG.m[i][j] + nG.m[j][i]);
+                H.m[i][j] = 0.5 * (nH.m[i][j] + nH.m[j][i]);
+            }
+        if (!isfinite(nrm)) return false;
+        if (last) { conv = true; break; }
+        // quadratic convergence: once the update is below 1e-10 relative, one more
+        // doubling step lands at rounding level
+        if (dH <= 1e-10 * nrm) last = true;
+    }
+    if (!conv) return false;
+    // K = (R + B'PB)^-1 B'PA   (lqr_controller.py:130-132)
+    double PB[3][2];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) PB[i][j] = H.m[i][0] * B[0][j] + H.m[i][1] * B[1][j] + H.m[i][2] * B[2][j];
+    double M[2][2], Nm[2][3];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+            M[a][b] = (a == b ? p.R[a] : 0.0) + B[0][a] * PB[0][b] + B[1][a] * PB[1][b] + B[2][a] * PB[2][b];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) Nm[a][j] = PB[0][a] * A.m[0][j] + PB[1][a] * A.m[1][j] + PB[2][a] * A.m[2][j];
+    const double id = 1.0 / (M[0][0] * M[1][1] - M[0][1] * M[1][0]);
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        K[j] = (M[1][1] * Nm[0][j] - M[0][1] * Nm[1][j]) * id;
+        K[3 + j] = (M[0][0] * Nm[1][j] - M[1][0] * Nm[0][j]) * id;
+    }
+    if (Pout) *Pout = H;
+    return isfinite(K[0] + K[1] + K[2] + K[3] + K[4] + K[5]);
+}
+
+__global__ __launch_bounds__(256) void lqr_control_kernel(LqrDevParams p, int64_t B, const double *x,
+                                                          const double *x_ref, int xref_stride,
+                                                          const double *u_ref, int uref_stride,
+                                                          RmpcLqrCache *cache, double *u_out,
+                                                          double *err_out, double *K_out,
+                                                          double *P_out, int32_t *status,
+                                                          const int32_t *index, const int32_t *count) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t n = index ? (int64_t)*count : B;
+    if (t >= n) return;
+    const int64_t b = index ? (int64_t)index[t] : t;
+    const double *xb = x + 3 * b;
+    const double *xr = x_ref + (size_t)xref_stride * b;
+    const double *ur = u_ref + (size_t)uref_stride * b;
+    const double v = ur[0], th = xr[2];
+    double K[6];
+    int st = RMPC_OPTIMAL;
+    bool hit = false;
+    if (cache && p.use_cache) {                      // lqr_controller.py:112-114
+        const RmpcLqrCache &cb = cache[b];
+        if (cb.valid && fabs(v - cb.last_v) < 1e-6 && fabs(th - cb.last_theta) < 1e-6) {
+#pragma unroll
+            for (int i = 0; i < 6; i++) K[i] = cb.K[i];
+            hit = true;
+        }
+    }
+    if (!hit) {
+        const double vg = fabs(v) < 1e-6 ? 0.01 : v;  // :120-122
+        M3 P;
+        if (!lqr_gain(p, vg, th, K, P_out ? &P : nullptr)) {
+            K[0] = 1; K[1] = 0; K[2] = 0; K[3] = 0; K[4] = 0; K[5] = 1;   // :137-140
+            st = RMPC_DARE_FALLBACK;
+        } else if (P_out) {
+#pragma unroll
+            for (int i = 0; i < 3; i++)
+#pragma unroll
+                for (int j = 0; j < 3; j++) P_out[9 * b + 3 * i + j] = P.m[i][j];
+        }
+        if (cache) {
+            RmpcLqrCache &cb = cache[b];
+#pragma unroll
+            for (int i = 0; i < 6; i++) cb.K[i] = K[i];
+            cb.last_v = v;
+            cb.last_theta = th;
+            cb.valid = 1;
+        }
+    }
+    // compute_control (:175-187)
+    const double e0 = xb[0] - xr[0], e1 = xb[1] - xr[1], e2 = wrap_pi(xb[2] - xr[2]);
+    const double u0 = ur[0] + -(K[0] * e0 + K[1] * e1 + K[2] * e2);
+    const double u1 = ur[1] + -(K[3] * e0 + K[4] * e1 + K[5] * e2);
+    u_out[2 * b] = clampv(u0, -p.v_max, p.v_max);
+    u_out[2 * b + 1] = clampv(u1, -p.omega_max, p.omega_max);
+    if (err_out) {
+        err_out[3 * b] = e0;
+        err_out[3 * b + 1] = e1;
+        err_out[3 * b + 2] = e2;
+    }
+    if (K_out)
+#pragma unroll
+        for (int i = 0; i < 6; i++) K_out[6 * b + i] = K[i];
+    if (status) status[b] = st;
+}
+
+__global__ __launch_bounds__(256) void lqr_gain_kernel(LqrDevParams p, int64_t B, const double *v_r,
+                                                       const double *theta_r, int guard,
+                                                       double *K_out, double *P_out, int32_t *status) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    double v = v_r[b];
+    if (guard && fabs(v) < 1e-6) v = 0.01;
+    double K[6];
+    M3 P;
+    const bool ok = lqr_gain(p, v, theta_r[b], K, &P);
+    if (!ok) { K[0] = 1; K[1] = 0; K[2] = 0; K[3] = 0; K[4] = 0; K[5] = 1; }
+#pragma unroll
+    for (int i = 0; i < 6; i++) K_out[6 * b + i] = K[i];
+    if (P_out)
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) P_out[9 * b + 3 * i + j] = ok ? P.m[i][j] : NAN;
+    if (status) status[b] = ok ? RMPC_OPTIMAL : RMPC_DARE_FALLBACK;
+}
+
+}  // namespace rmpc
+
+using namespace rmpc;
+
+hipError_t rmpc_launch_lqr_control(const LqrDevParams &p, int64_t B, const double *x,
+                                   const double *x_ref, int xref_stride, const double *u_ref,
+                                   int uref_stride, RmpcLqrCache *cache, double *u_out,
+                                   double *err_out, double *K_out, double *P_out, int32_t *status,
+                                   const int32_t *index, const int32_t *count, hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    const int threads = 256;
+    hipLaunchKernelGGL(lqr_control_kernel, dim3((unsigned)((B + threads - 1) / threads)), dim3(threads), 0,
+                       stream, p, B, x, x_ref, xref_stride, u_ref, uref_stride, cache, u_out, err_out,
+                       K_out, P_out, status, index, count);
+    return hipGetLastError();
+}
+
+hipError_t rmpc_launch_lqr_gain(const LqrDevParams &p, int64_t B, const double *v_r,
+                                const double *theta_r, int guard, double *K_out, double *P_out,
+                                int32_t *status, hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    const int threads = 256;
+    hipLaunchKernelGGL(lqr_gain_kernel, dim3((unsigned)((B + threads - 1) / threads)), dim3(threads), 0,
+                       stream, p, B, v_r, theta_r, guard, K_out, P_out, status);
+    return hipGetLastError();
+}

@@ -1,0 +1,210 @@
+// rmpc_misc.hip -- risk metrics, hybrid LQR/MPC switch with branch compaction, unicycle
+// plant step and Figure-8 reference generation on CDNA4 (gfx950).  One lane per robot.
+#include "rmpc_device.h"
+#include "rmpc_internal.h"
+
+namespace rmpc {
+
+// risk_metrics.py:84-129
+__device__ __forceinline__ double distance_risk(const RiskDevParams &p, double px, double py,
+                                                const double *obs, int no, double *min_d, int *nid) {
+    double md = INFINITY, mr = 0.0;
+    int id = -1;
+    for (int i = 0; i < no; i++) {
+        const double dx = px - obs[3 * i], dy = py - obs[3 * i + 1];
+        const double d = sqrt(dx * dx + dy * dy) - obs[3 * i + 2];
+        if (d < md) { md = d; id = i; }
+        double r;
+        if (d <= p.d_safe) r = 1.0;
+        else if (d >= p.d_trigger) r = 0.0;
+        else r = 1.0 - (d - p.d_safe) / (p.d_trigger - p.d_safe);
+        mr = fmax(mr, r);
+    }
+    *min_d = md;
+    *nid = id;
+    return mr;
+}
+
+// risk_metrics.py:131-171
+__device__ __forceinline__ double predictive_risk(const RiskDevParams &p, const double *pred, int n,
+                                                  const double *obs, int no) {
+    if (no == 0 || n == 0) return 0.0;
+    double sev = 0.0;
+    for (int k = 0; k < n; k++) {
+        const double px = pred[3 * k], py = pred[3 * k + 1];
+        for (int i = 0; i < no; i++) {
+            const double dx = px - obs[3 * i], dy = py - obs[3 * i + 1];
+            const double d = sqrt(dx * dx + dy * dy) - obs[3 * i + 2];
+            if (d < p.d_safe) {
+                const double tw = 1.0 - ((double)k / (double)n) * 0.5;
+                sev += tw * ((p.d_safe - d) / p.d_safe);
+            }
+        }
+    }
+    return fmin(1.0, sev / (double)(n * no) * 5.0);
+}
+
+__device__ __forceinline__ void normalise_weights(const RiskDevParams &p, double *al, double *be) {
+    const double tot = p.alpha + p.beta;          // risk_metrics.py:79-82
+    *al = p.alpha / tot;
+    *be = p.beta / tot;
+}
+
+__global__ __launch_bounds__(256) void risk_kernel(RiskDevParams p, int64_t B, const double *x,
+                                                   const double *pred, int n_pred,
+                                                   const double *obs, int no, double *out,
+                                                   uint8_t *use_mpc, int32_t *level) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    double md;
+    int nid;
+    const double dr = no ? distance_risk(p, x[3 * b], x[3 * b + 1], obs, no, &md, &nid) : 0.0;
+    if (!no) { md = INFINITY; nid = -1; }
+    const double pr = pred ? predictive_risk(p, pred + (size_t)3 * n_pred * b, n_pred, obs, no) : 0.0;
+    double al, be;
+    normalise_weights(p, &al, &be);
+    const double c = al * dr + be * pr;           // :198
+    int lv = c < p.th_low ? 0 : (c < p.th_med ? 1 : (c < p.th_high ? 2 : 3));
+    out[5 * b] = dr;
+    out[5 * b + 1] = pr;
+    out[5 * b + 2] = c;
+    out[5 * b + 3] = md;
+    out[5 * b + 4] = (double)nid;
+    if (use_mpc) use_mpc[b] = c >= p.th_low;     // :212
+    if (level) level[b] = lv;
+}
+
+// run_simulation.py:528-548: risk (no predicted states), 10-step dwell hysteresis, switch
+// bookkeeping; robots are compacted into per-branch index lists so that each branch runs
+// as full waves of one kernel (no LQR/MPC divergence inside a wave).
+__global__ __launch_bounds__(256) void hybrid_decide_kernel(RiskDevParams p, int64_t B, const double *x,
+                                                            const double *obs, int no, int32_t *prev_ctrl,
+                                                            int32_t *steps_since, uint8_t *used_mpc,
+                                                            double *risk_out, int32_t *idx_lqr,
+                                                            int32_t *idx_mpc, int32_t *counts) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    double md;
+    int nid;
+    const double dr = no ? distance_risk(p, x[3 * b], x[3 * b + 1], obs, no, &md, &nid) : 0.0;
+    double al, be;
+    normalise_weights(p, &al, &be);
+    const double c = al * dr + be * 0.0;
+    const bool rec = c >= p.th_low;
+    const int prev = prev_ctrl[b];
+    int since = steps_since[b];
+    bool mpc;
+    if (since >= p.min_dwell) mpc = rec;                    // :533-534
+    else mpc = prev >= 0 ? (prev == 1) : rec;              // :536-537
+    const int cur = mpc ? 1 : 0;
+    if (prev >= 0 && cur != prev) since = 0;                // :542-546
+    else since += 1;
+    prev_ctrl[b] = cur;
+    steps_since[b] = since;
+    used_mpc[b] = (uint8_t)mpc;
+    if (risk_out) risk_out[b] = c;
+    // compaction (order inside a list is irrelevant: robots are independent)
+    if (mpc) idx_mpc[atomicAdd(&counts[1], 1)] = (int32_t)b;
+    else idx_lqr[atomicAdd(&counts[0], 1)] = (int32_t)b;
+}
+
+// differential_drive.py:111-172
+__global__ __launch_bounds__(256) void plant_kernel(int64_t B, const double *x, const double *u, double dt,
+                                                    double v_max, double omega_max, int method,
+                                                    double *xn) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const double v = clampv(u[2 * b], -v_max, v_max), w = clampv(u[2 * b + 1], -omega_max, omega_max);
+    const double x0 = x[3 * b], x1 = x[3 * b + 1], x2 = x[3 * b + 2];
+    double n0, n1, n2;
+    if (method == 0) {
+        n0 = x0 + dt * (v * cos(x2));
+        n1 = x1 + dt * (v * sin(x2));
+        n2 = x2 + dt * w;
+    } else {
+        const double k10 = v * cos(x2), k11 = v * sin(x2), k12 = w;
+        const double t2 = x2 + 0.5 * dt * k12;
+        const double k20 = v * cos(t2), k21 = v * sin(t2), k22 = w;
+        const double t3 = x2 + 0.5 * dt * k22;
+        const double k30 = v * cos(t3), k31 = v * sin(t3), k32 = w;
+        const double t4 = x2 + dt * k32;
+        const double k40 = v * cos(t4), k41 = v * sin(t4), k42 = w;
+        const double h = dt / 6.0;
+        n0 = x0 + h * (k10 + 2 * k20 + 2 * k30 + k40);
+        n1 = x1 + h * (k11 + 2 * k21 + 2 * k31 + k41);
+        n2 = x2 + h * (k12 + 2 * k22 + 2 * k32 + k42);
+    }
+    xn[3 * b] = n0;
+    xn[3 * b + 1] = n1;
+    xn[3 * b + 2] = wrap_pi(n2);
+}
+
+// reference_generator.py:86-172 evaluated at t0[b] + i*dt
+__device__ __forceinline__ double heading8(double A, double a, double t) {
+    const double dpx = a * A * cos(a * t);
+    const double c = cos(a * t), s = sin(a * t);
+    const double dpy = a * A * (c * c - s * s);
+    return atan2(dpy, dpx);
+}
+
+__global__ __launch_bounds__(256) void figure8_kernel(int64_t B, const double *t0, int rows, double A, double a,
+                                                      double dt, double *xr, double *ur) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= B * rows) return;
+    const int64_t b = g / rows;
+    const int i = (int)(g % rows);
+    const double t = t0[b] + (double)i * dt;
+    const double s = sin(a * t), c = cos(a * t);
+    const double px = A * s, py = A * s * c;
+    const double dpx = a * A * c, dpy = a * A * (c * c - s * s);
+    const double th = atan2(dpy, dpx);
+    const double v = sqrt(dpx * dpx + dpy * dpy);
+    const double om = wrap_pi(heading8(A, a, t + dt) - th) / dt;
+    xr[3 * g] = px;
+    xr[3 * g + 1] = py;
+    xr[3 * g + 2] = th;
+    ur[2 * g] = v;
+    ur[2 * g + 1] = om;
+}
+
+}  // namespace rmpc
+
+using namespace rmpc;
+
+static inline unsigned nblk(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
+
+hipError_t rmpc_launch_risk(const RiskDevParams &p, int64_t B, const double *x, const double *pred,
+                            int n_pred, const double *obstacles, int n_obs, double *out,
+                            uint8_t *use_mpc, int32_t *level, hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(risk_kernel, dim3(nblk(B, 256)), dim3(256), 0, stream, p, B, x, pred, n_pred,
+                       obstacles, n_obs, out, use_mpc, level);
+    return hipGetLastError();
+}
+
+hipError_t rmpc_launch_hybrid_decide(const RiskDevParams &p, int64_t B, const double *x,
+                                     const double *obstacles, int n_obs, int32_t *prev_ctrl,
+                                     int32_t *steps_since, uint8_t *used_mpc, double *risk_out,
+                                     int32_t *idx_lqr, int32_t *idx_mpc, int32_t *counts,
+                                     hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(hybrid_decide_kernel, dim3(nblk(B, 256)), dim3(256), 0, stream, p, B, x, obstacles,
+                       n_obs, prev_ctrl, steps_since, used_mpc, risk_out, idx_lqr, idx_mpc, counts);
+    return hipGetLastError();
+}
+
+hipError_t rmpc_launch_plant(int64_t B, const double *x, const double *u, double dt, double v_max,
+                             double omega_max, int method, double *x_next, hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(plant_kernel, dim3(nblk(B, 256)), dim3(256), 0, stream, B, x, u, dt, v_max,
+                       omega_max, method, x_next);
+    return hipGetLastError();
+}
+
+hipError_t rmpc_launch_figure8(int64_t B, const double *t0, int rows, double A, double a,
+                               double dt, double *x_refs, double *u_refs, hipStream_t stream) {
+    if (B <= 0 || rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(figure8_kernel, dim3(nblk(B * rows, 256)), dim3(256), 0, stream, B, t0, rows, A, a,
+                       dt, x_refs, u_refs);
+    return hipGetLastError();
+}

@@ -1,0 +1,16 @@
+"""rmpc -- MI355X batched MPC / LQR solve path (drop-in for the reference's controllers).
+
+Reference interface mirrored (hybrid_controller/controllers/*.py):
+  MPCController, MPCSolution, Obstacle   mpc_controller.py
+  LQRController                          lqr_controller.py
+  RiskMetrics, RiskAssessment            risk_metrics.py
+All compute runs in librmpc.so (HIP, gfx950); there is no CPU fallback.
+"""
+from ._native import RmpcError, load  # noqa: F401
+from .lqr_controller import LQRController  # noqa: F401
+from .mpc_controller import MPCController, MPCSolution, Obstacle  # noqa: F401
+from .risk_metrics import RiskAssessment, RiskMetrics  # noqa: F401
+from . import batch, params  # noqa: F401
+
+__all__ = ["MPCController", "MPCSolution", "Obstacle", "LQRController", "RiskMetrics",
+           "RiskAssessment", "RmpcError", "batch", "params", "load"]

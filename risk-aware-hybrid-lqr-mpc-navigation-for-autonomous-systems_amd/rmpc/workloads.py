@@ -1,0 +1,52 @@
+"""Synthetic BASELINE workloads and the batch split across ranks.
+
+Robot i of a global batch of B robots follows the Figure-8 (A=2, a=0.5, dt=0.02) with time
+offset t0_i = (i / B) * 2*pi/a (one full period over the batch) and starts at
+x_ref(t0_i) + N(0, diag(.05^2, .05^2, .1^2)).  Noise is drawn per robot from a counter-based
+generator keyed on (seed, i), so any contiguous shard of the batch is reproduced exactly
+by the rank that owns it -- no data-path collective is needed to split the batch.
+"""
+import numpy as np
+
+PERIOD = 2 * np.pi / 0.5
+
+DEFAULT_OBS = [(1.0, 0.5, 0.2), (-0.5, -1.0, 0.25), (1.5, -0.3, 0.15)]     # run_simulation.py:215-219
+UNION8_OBS = DEFAULT_OBS + [(-1.5, 0.5, 0.2), (0.0, 0.8, 0.15), (1.5, 0.8, 0.2),
+                            (-0.8, -0.7, 0.15), (-0.3, -1.2, 0.15)]          # :191-212
+
+CONFIGS = {
+    # name: (horizon, obstacles, global batch at N=1, seed, what)
+    "cfg2": dict(N=0, obs=[], B=4096, seed=0, what="LQR DARE+gain+apply, fp64"),
+    "cfg3": dict(N=20, obs=DEFAULT_OBS, B=65536, seed=1, what="MPC QP N=20, 3 obstacles, fp64"),
+    "cfg4": dict(N=30, obs=UNION8_OBS, B=32768, seed=2, what="MPC QP N=30, 8 obstacles"),
+    "cfg5": dict(N=20, obs=DEFAULT_OBS, B=65536, seed=3, what="hybrid LQR/MPC step, N=20"),
+}
+
+
+def shard(B_total, world, rank):
+    """Contiguous split: rank r owns [r*B/W, (r+1)*B/W)."""
+    lo = (B_total * rank) // world
+    hi = (B_total * (rank + 1)) // world
+    return lo, hi
+
+
+def t0_offsets(lo, hi, B_total):
+    return (np.arange(lo, hi, dtype=np.float64) / B_total) * PERIOD
+
+
+def _noise_aligned(lo, hi, seed, sigma=(0.05, 0.05, 0.1)):
+    """Per-robot N(0, sigma^2) keyed on (seed, global index); lo must be 65536-aligned."""
+    out = np.empty((hi - lo, 3))
+    for i0 in range(lo, hi, 65536):
+        i1 = min(hi, i0 + 65536)
+        ss = np.random.SeedSequence([seed, i0 // 65536])
+        z = np.random.default_rng(ss).standard_normal((65536, 3))
+        out[i0 - lo:i1 - lo] = z[: i1 - i0] * np.asarray(sigma)
+    return out
+
+
+def noise_for(lo, hi, seed, sigma=(0.05, 0.05, 0.1)):
+    """Noise for an arbitrary [lo, hi) that may start inside a 65536-block."""
+    b0 = (lo // 65536) * 65536
+    full = _noise_aligned(b0, hi, seed, sigma)
+    return full[lo - b0:]

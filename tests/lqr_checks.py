@@ -1,0 +1,26 @@
+"""Shared LQR gain parity check (CPU port and GPU kernel vs the reference's SciPy gains)."""
+import numpy as np
+
+from oracle.plant import discrete_model_explicit
+
+
+def dare_residual(P, v, t, Q, R, dt=0.02, guard=True):
+    if guard and abs(v) < 1e-6:
+        v = 0.01
+    A, B = discrete_model_explicit(v, t, dt)
+    r = A.T @ P @ A - P - A.T @ P @ B @ np.linalg.solve(R + B.T @ P @ B, B.T @ P @ A) + Q
+    return np.abs(r).max() / np.abs(P).max()
+
+
+def assert_gains_match(grid, K, P, K_ref, P_ref, Q, R):
+    """Tolerance follows the DARE's conditioning: on the operating range (|v_r| >= 0.1)
+    |dK| <= 1e-10; at the near-uncontrollable guard points (|v_r| <= 0.01, ||P|| up to
+    5e5) |dK| <= 1e-7 * max(1, |K|).  In both cases our DARE residual must not exceed
+    SciPy's (QZ) residual -- i.e. the SDA solution is at least as accurate."""
+    for i, (v, t) in enumerate(grid):
+        tol = 1e-10 if abs(v) >= 0.1 else 1e-7 * max(1.0, np.abs(K_ref[i]).max())
+        d = np.abs(K[i] - K_ref[i]).max()
+        assert d <= tol, (v, t, d, tol)
+        rs = dare_residual(P[i], v, t, Q, R)
+        rr = dare_residual(P_ref[i], v, t, Q, R)
+        assert rs <= max(2 * rr, 1e-15), (v, t, rs, rr)

@@ -1,0 +1,92 @@
+"""C-ABI surface checks that need no GPU: symbols, struct layout, error paths, params.yaml."""
+import ctypes as C
+import os
+import re
+import subprocess
+import textwrap
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+HEADER = os.path.join(ROOT, "include", "rmpc.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rmpc_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol(lib):
+    names = header_functions()
+    assert len(names) >= 15
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    from rmpc import _native
+    assert set(names) == set(_native.exported_symbols())
+
+
+def test_abi_version(lib):
+    assert lib.rmpc_abi_version() == 1
+
+
+def test_struct_layout_matches_header(tmp_path):
+    """Compile a probe against include/rmpc.h and compare sizeof/offsetof with ctypes."""
+    from rmpc import _native as n
+    probe = tmp_path / "probe.c"
+    probe.write_text(textwrap.dedent(f"""
+        #include <stdio.h>
+        #include <stddef.h>
+        #include "{HEADER}"
+        int main(void) {{
+          printf("%zu %zu %zu %zu\\n", sizeof(RmpcMpcParams), sizeof(RmpcLqrParams),
+                 sizeof(RmpcRiskParams), sizeof(RmpcLqrCache));
+          printf("%zu %zu %zu %zu\\n", offsetof(RmpcMpcParams, Q), offsetof(RmpcMpcParams, dt),
+                 offsetof(RmpcLqrParams, max_iter), offsetof(RmpcLqrCache, valid));
+          return 0; }}"""))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", str(probe), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    got = [int(v) for v in out]
+    want = [C.sizeof(n.MpcParams), C.sizeof(n.LqrParams), C.sizeof(n.RiskParams),
+            C.sizeof(n.LqrCache), n.MpcParams.Q.offset, n.MpcParams.dt.offset,
+            n.LqrParams.max_iter.offset, n.LqrCache.valid.offset]
+    assert got == want
+    assert n.LQR_CACHE_DTYPE.itemsize == C.sizeof(n.LqrCache)
+
+
+def test_null_context_is_rejected(lib):
+    from rmpc import _native as n
+    p = n.mpc_params(20, [15, 15, 50], [.1, .1], [30, 30, 40], .3, 5000., 2., 3., .02)
+    rc = lib.rmpc_mpc_solve_batch(None, C.byref(p), 1, None, None, 21, None, 21, None, 0, None,
+                                  None, None, None, None, None, None, None)
+    assert rc == -1
+    assert b"ctx" in lib.rmpc_last_error()
+    lp = n.lqr_params([15, 15, 8], [.1, .1], .02, 2., 3.)
+    assert lib.rmpc_lqr_control_batch(None, C.byref(lp), 1, None, None, None, None, None, None,
+                                      None, None, None) == -1
+    assert lib.rmpc_ctx_destroy(None) == 0
+
+
+def test_context_without_device_fails_loudly(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("device present")
+    from rmpc import _native as n
+    with pytest.raises(n.RmpcError):
+        n.context(0)
+
+
+def test_params_yaml_surface():
+    from rmpc import params
+    cfg = params.load_params(os.path.join(GOLDEN, "params.yaml"))
+    lk = params.lqr_kwargs(cfg)
+    mk = params.mpc_kwargs(cfg)
+    assert lk == dict(Q_diag=[10.0, 10.0, 1.0], R_diag=[0.1, 0.1], dt=0.02, v_max=1.0,
+                      omega_max=1.5)
+    assert mk["horizon"] == 10 and mk["slack_penalty"] == 1000.0 and mk["solver"] == "ECOS"
+    assert mk["P_diag"] == [20.0, 20.0, 2.0]
+    s = params.mpc_struct(cfg)
+    assert s.horizon == 10 and list(s.Q) == [10.0, 10.0, 1.0]

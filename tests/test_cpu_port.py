@@ -1,0 +1,51 @@
+"""The C restatement (oracle/c, the timed CPU baseline) against the numpy oracle."""
+import numpy as np
+import pytest
+
+from lqr_checks import assert_gains_match
+from oracle import cpu, figure8, mpc
+
+
+def _case(N, bs, obs, B, ltv=True, noise=(0.05, 0.05, 0.1), seed=0, vmax=2.0, wmax=3.0):
+    rng = np.random.default_rng(seed)
+    t0 = rng.uniform(0, 4 * np.pi, B)
+    xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, t0, N + 1)
+    x0 = xr[:, 0] + rng.normal(0, noise, (B, 3))
+    return x0, xr, ur
+
+
+@pytest.mark.parametrize("N,bs,scen,ltv,noise,seed", [
+    (6, 2, "default", True, (0.3, 0.3, 0.5), 0),
+    (20, 1, "default", True, (0.3, 0.3, 0.5), 3),
+    (10, 3, "dense", True, (0.2, 0.2, 0.3), 5),
+    (20, 1, "default", False, (0.2, 0.2, 0.3), 7),
+])
+def test_cpu_port_matches_oracle(N, bs, scen, ltv, noise, seed):
+    obs = mpc.scenario_obstacles(scen)
+    B = 40
+    x0, xr, ur = _case(N, bs, obs, B, ltv, noise, seed)
+    p = cpu.mpc_params(N, (15, 15, 50), (.1, .1), (30, 30, 40), 0.3, 5000., 2., 3., 0.02,
+                       block_size=bs, ltv=ltv)
+    sc = np.full(B, 3, np.int32)
+    out = cpu.mpc_solve_batch(p, x0, xr, ur, obs, step_count=sc)
+    assert np.all(out["status"] == 0)
+    c = mpc.MPCController(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000., 2., 3., 0.02,
+                          "OSQP", bs)
+    for b in range(B):
+        c._step_count = 3
+        s = c.solve_with_ltv(x0[b], xr[b], ur[b], obs) if ltv else c.solve(x0[b], xr[b], ur[b], obs)
+        np.testing.assert_allclose(out["u_seq"][b], s.control_sequence, atol=1e-9, rtol=0)
+        np.testing.assert_allclose(out["x_pred"][b], s.predicted_states, atol=1e-9, rtol=0)
+        assert abs(out["cost"][b] - s.cost) <= 1e-9 * max(1.0, abs(s.cost))
+        assert bool(out["slack_used"][b]) == s.slack_used
+    if ltv:
+        assert np.all(sc == 4)
+
+
+def test_cpu_port_lqr_gain_matches_reference(golden):
+    d = golden("lqr.npz")
+    p = cpu.lqr_params(d["Q_sim"], d["R"], 0.02, 2.0, 3.0)
+    K, P, st = cpu.lqr_gain_batch(p, d["grid"][:, 0], d["grid"][:, 1])
+    assert np.all(st == 0)
+    assert_gains_match(d["grid"], K, P, d["K_sim"], d["P_sim"], np.diag(d["Q_sim"]),
+                       np.diag(d["R"]))

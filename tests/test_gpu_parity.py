@@ -1,0 +1,321 @@
+"""GPU parity: librmpc.so (HIP, gfx950) against the CPU oracle and the reference's own
+golden vectors / logged runs.  Every call goes through the C-ABI.
+
+Tolerances (written per test): fp64 MPC vs the exact-QP oracle |du|, |dx| <= 1e-9;
+LQR gains conditioning-aware (tests/lqr_checks.py); LQR closed loop <= 1e-10;
+risk / plant / Figure-8 <= 1e-12 (ulp-level differences of device libm vs numpy).
+"""
+import numpy as np
+import pytest
+
+from lqr_checks import assert_gains_match
+from oracle import cpu, figure8, lqr as olqr, mpc as ompc, plant as oplant, risk as orisk, sims
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rm(gpu_lib):
+    import rmpc
+    return rmpc
+
+
+def _workload(N, B, seed, noise=(0.05, 0.05, 0.1), t0=None):
+    rng = np.random.default_rng(seed)
+    if t0 is None:
+        t0 = rng.uniform(0, 4 * np.pi, B)
+    xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, t0, N + 1)
+    x0 = xr[:, 0] + rng.normal(0, noise, (B, 3))
+    return x0, xr, ur
+
+
+# ------------------------------------------------------------------------------------ LQR
+def test_lqr_gain_grid_matches_reference(rm, golden):
+    d = golden("lqr.npz")
+    for tag in ("sim", "default"):
+        p = rm._native.lqr_params(d[f"Q_{tag}"], d["R"], 0.02, 2.0, 3.0)
+        K, P, st = rm.batch.lqr_gain_batch(p, d["grid"][:, 0], d["grid"][:, 1], guard=True)
+        assert np.all(st == 0)
+        assert_gains_match(d["grid"], K, P, d[f"K_{tag}"], d[f"P_{tag}"],
+                           np.diag(d[f"Q_{tag}"]), np.diag(d["R"]))
+
+
+def test_lqr_control_matches_reference(rm, golden):
+    d = golden("lqr.npz")
+    c = rm.LQRController([15.0, 15.0, 8.0], [0.1, 0.1], 0.02, 2.0, 3.0)
+    for x, xr, ur, u, e in zip(d["ctl_x"], d["ctl_xref"], d["ctl_uref"], d["ctl_u"], d["ctl_e"]):
+        uu, ee = c.compute_control_at_operating_point(x, xr, ur)
+        np.testing.assert_allclose(uu, u, atol=1e-11, rtol=0)
+        np.testing.assert_allclose(ee, e, atol=1e-15, rtol=0)
+
+
+def test_lqr_closed_loop_drop_in_matches_log(rm, golden):
+    """run_simulation.py --mode lqr with the HIP LQRController swapped in (999 steps)."""
+    d = golden("lqr_closed_loop.npz")
+    g = figure8.Figure8(2.0, 0.5, 0.02)
+    tab = g.generate(20.0)
+    c = rm.LQRController([15.0, 15.0, 8.0], [0.1, 0.1], 0.02, 2.0, 3.0)
+    x = g.reference_at_index(0)[0].copy()
+    us = []
+    for k in range(len(tab) - 1):
+        xr, ur = g.reference_at_index(k)
+        u, _ = c.compute_control_at_operating_point(x, xr, ur)
+        x = oplant.simulate_step(x, u, 0.02, 2.0, 3.0)
+        us.append(u)
+    np.testing.assert_allclose(np.array(us), d["log_controls"], atol=1e-10, rtol=0)
+
+
+def test_lqr_batch_cfg2_matches_scipy_and_cache(rm):
+    """BASELINE config 2 workload (B=4096, Q=[15,15,8]) vs SciPy DARE per robot."""
+    B = 4096
+    t0 = (np.arange(B) / B) * (2 * np.pi / 0.5)
+    x0, xr, ur = _workload(0, B, 0, t0=t0)
+    p = rm._native.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0)
+    cache = np.zeros(B, rm._native.LQR_CACHE_DTYPE)
+    u, e, K, _, st = rm.batch.lqr_control_batch(p, x0, xr[:, 0], ur[:, 0], cache=cache,
+                                                want_K=True)
+    assert np.all(st == 0) and np.all(cache["valid"] == 1)
+    Q, R = np.diag([15.0, 15, 8]), np.diag([0.1, 0.1])
+    c = olqr.LQRController([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0)
+    for b in range(0, B, 7):
+        Kr, _, ok = olqr.dare_gain(ur[b, 0, 0], xr[b, 0, 2], Q, R, 0.02)
+        np.testing.assert_allclose(K[b], Kr, atol=1e-10, rtol=0)
+        c.K = None
+        ur_, _ = c.compute_control_at_operating_point(x0[b], xr[b, 0], ur[b, 0])
+        np.testing.assert_allclose(u[b], ur_, atol=1e-10, rtol=0)
+    # second call with the same operating points: every robot hits its cache (:112-114)
+    u2, _, K2, _, _ = rm.batch.lqr_control_batch(p, x0 + 0.01, xr[:, 0], ur[:, 0], cache=cache,
+                                                 want_K=True)
+    np.testing.assert_array_equal(K2, K)
+
+
+# ------------------------------------------------------------------------------------ MPC
+def test_mpc_ltv_drop_in_vs_logged_osqp(rm, golden):
+    """The 200 solves of run_simulation.py --mode mpc (N=6, bs=2, rho=5000) through the
+    HIP MPCController, fed the logged states; step counter advances as in the sim."""
+    d = golden("mpc_log_014109.npz")
+    g = figure8.Figure8(2.0, 0.5, 0.02)
+    g.generate(20.0)
+    kw = dict(horizon=6, Q_diag=[15, 15, 50], R_diag=[.1, .1], P_diag=[30, 30, 40], d_safe=0.3,
+              slack_penalty=5000.0, v_max=2.0, omega_max=3.0, dt=0.02, solver="OSQP",
+              block_size=2)
+    c = rm.MPCController(**kw)
+    oc = ompc.MPCController(**kw)
+    err_log, err_orc, slack = [], [], []
+    for k, x0, u0 in zip(d["k"], d["x0"], d["u0"]):
+        xr, ur = g.segment(int(k), 7)
+        s = c.solve_with_ltv(x0, xr, ur, [rm.Obstacle(*o) for o in ompc.default_obstacles()])
+        so = oc.solve_with_ltv(x0, xr, ur, ompc.default_obstacles())
+        assert s.status == "optimal"
+        err_log.append(np.abs(s.optimal_control - u0).max())
+        err_orc.append(max(np.abs(s.control_sequence - so.control_sequence).max(),
+                           np.abs(s.predicted_states - so.predicted_states).max()))
+        slack.append(s.slack_used)
+        assert s.slack_used == so.slack_used
+        assert abs(s.cost - so.cost) <= 1e-9 * max(1.0, abs(so.cost))
+    err_log, err_orc, slack = map(np.array, (err_log, err_orc, slack))
+    assert c._step_count == 200
+    assert np.all(err_orc <= 1e-9)
+    assert (err_log <= 1e-9).sum() >= 189 and np.all(err_log[~slack] <= 1e-9)
+    assert np.all(err_log <= 2e-3)        # OSQP's own error on slack-active solves
+
+
+CASES = [  # (N, bs, scenario, ltv, noise, seed, B)
+    (20, 1, "default", True, (0.05, 0.05, 0.1), 1, 48),      # BASELINE config 3
+    (20, 1, "default", True, (0.4, 0.4, 0.6), 2, 48),        # obstacles active
+    (30, 1, "union8", True, (0.1, 0.1, 0.2), 3, 24),         # config 4 sizes (fp64)
+    (6, 2, "default", True, (0.3, 0.3, 0.5), 4, 48),         # reference sim config
+    (10, 3, "dense", True, (0.2, 0.2, 0.3), 5, 32),          # ragged last block
+    (20, 1, "default", False, (0.2, 0.2, 0.3), 6, 32),       # LTI solve()
+    (1, 1, "corridor", True, (0.1, 0.1, 0.1), 7, 16),        # N = 1
+]
+
+
+@pytest.mark.parametrize("N,bs,scen,ltv,noise,seed,B", CASES)
+def test_mpc_kernel_matches_exact_qp_oracle(rm, N, bs, scen, ltv, noise, seed, B):
+    obs = ompc.union8_obstacles() if scen == "union8" else ompc.scenario_obstacles(scen)
+    x0, xr, ur = _workload(N, B, seed, noise)
+    p = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                              0.02, block_size=bs, ltv=ltv)
+    sc = np.full(B, 4, np.int32)
+    out = rm.batch.mpc_solve_batch(p, x0, xr, ur, obs, step_count=sc if ltv else None)
+    assert np.all(out["status"] == 0)
+    oc = ompc.MPCController(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                            0.02, "OSQP", bs)
+    for b in range(B):
+        oc._step_count = 4
+        s = oc.solve_with_ltv(x0[b], xr[b], ur[b], obs) if ltv else oc.solve(x0[b], xr[b], ur[b], obs)
+        np.testing.assert_allclose(out["u_seq"][b], s.control_sequence, atol=1e-9, rtol=0)
+        np.testing.assert_allclose(out["x_pred"][b], s.predicted_states, atol=1e-9, rtol=0)
+        np.testing.assert_allclose(out["u0"][b], s.optimal_control, atol=1e-9, rtol=0)
+        assert abs(out["cost"][b] - s.cost) <= 1e-9 * max(1.0, abs(s.cost))
+        assert bool(out["slack_used"][b]) == s.slack_used
+    if ltv:
+        assert np.all(sc == 5)
+
+
+def test_mpc_full_config3_vs_cpu_port(rm):
+    """BASELINE config 3 at full size (B=65536, N=20, 3 obstacles): every robot against the
+    C restatement; run twice to check determinism."""
+    B, N = 65536, 20
+    t0 = (np.arange(B) / B) * (2 * np.pi / 0.5)
+    x0, xr, ur = _workload(N, B, 1, t0=t0)
+    obs = ompc.default_obstacles()
+    p = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+    out = rm.batch.mpc_solve_batch(p, x0, xr, ur, obs)
+    out2 = rm.batch.mpc_solve_batch(p, x0, xr, ur, obs)
+    for k in ("u0", "u_seq", "x_pred", "cost", "status", "iters"):
+        np.testing.assert_array_equal(out[k], out2[k])
+    cp = cpu.mpc_params(N, (15, 15, 50), (.1, .1), (30, 30, 40), 0.3, 5000., 2., 3., 0.02)
+    ref = cpu.mpc_solve_batch(cp, x0, xr, ur, obs, threads=8)
+    ok = out["status"] == 0
+    assert ok.mean() >= 0.9999
+    assert np.all(out["status"] <= 1)
+    d = np.abs(out["u_seq"] - ref["u_seq"]).max(axis=(1, 2))
+    assert np.all(d[ok & (ref["status"] == 0)] <= 1e-9), d.max()
+    assert np.array_equal(out["slack_used"][ok], ref["slack_used"][ok])
+
+
+def test_mpc_edge_cases(rm):
+    obs = ompc.default_obstacles()
+    oc = ompc.MPCController(6, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                            0.02, "OSQP", 2)
+    p = rm._native.mpc_params(6, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                              0.02, block_size=2)
+    # empty batch
+    out = rm.batch.mpc_solve_batch(p, np.zeros((0, 3)), np.zeros((0, 7, 3)), np.zeros((0, 7, 2)), obs)
+    assert out["u0"].shape == (0, 2)
+    x0, xr, ur = _workload(6, 6, 11, (0.1, 0.1, 0.2))
+    # heading crossing +-pi inside the horizon (np.unwrap), x0 heading 4 pi off (wrap)
+    xr[0, :, 2] = np.linspace(3.05, 3.05 + 0.3, 7)
+    xr[0, :, 2] = (xr[0, :, 2] + np.pi) % (2 * np.pi) - np.pi
+    x0[1, 2] += 4 * np.pi
+    ur[2, :, 0] = 0.004                       # |v_r| <= 0.01 -> 0.1 (mpc_controller.py:425)
+    xr[3, 2, :2] = obs[0][:2]                 # reference on an obstacle centre: row skipped
+    xr[4, :, :2] = np.array(obs[1][:2]) + 0.25   # deep inside d_safe: slack active
+    sc = np.zeros(6, np.int32)
+    out = rm.batch.mpc_solve_batch(p, x0, xr, ur, obs, step_count=sc)
+    assert np.all(out["status"] == 0)
+    for b in range(6):
+        oc._step_count = 0
+        s = oc.solve_with_ltv(x0[b], xr[b], ur[b], obs)
+        np.testing.assert_allclose(out["u_seq"][b, 1:], s.control_sequence[1:], atol=1e-9)
+        np.testing.assert_allclose(out["u0"][b], s.optimal_control, atol=1e-9)   # ramp applied
+    assert bool(out["slack_used"][4])
+    # non-finite input -> fallback law (mpc_controller.py:316-343), status fallback
+    x0n = x0.copy()
+    x0n[5, 0] = np.nan
+    out = rm.batch.mpc_solve_batch(p, x0n, xr, ur, obs)
+    assert out["status"][5] == 2 and np.isinf(out["cost"][5])
+    assert np.all(out["status"][:5] == 0)
+    # LTI with short (ragged) references: padded with the last row (:172-183)
+    pl = rm._native.mpc_params(6, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                               0.02, ltv=False)
+    out = rm.batch.mpc_solve_batch(pl, x0[:3], xr[:3, :3], ur[:3, :2], obs)
+    for b in range(3):
+        s = oc.solve(x0[b], xr[b, :3], ur[b, :2], obs)
+        np.testing.assert_allclose(out["u_seq"][b], s.control_sequence, atol=1e-9)
+
+
+def test_mpc_ramp_and_step_count(rm):
+    """Cold-start omega ramp (mpc_controller.py:502-507) through the class API."""
+    c = rm.MPCController(horizon=6, Q_diag=[15, 15, 50], P_diag=[30, 30, 40], v_max=2.0,
+                         omega_max=3.0, slack_penalty=5000.0, block_size=2)
+    oc = ompc.MPCController(6, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                            0.02, "OSQP", 2)
+    g = figure8.Figure8(2.0, 0.5, 0.02)
+    g.generate(20.0)
+    xr, ur = g.segment(100, 7)
+    x0 = xr[0] + np.array([0.0, 0.0, 1.2])      # large heading error -> omega saturates
+    for i in range(12):
+        s = c.solve_with_ltv(x0, xr, ur, [])
+        so = oc.solve_with_ltv(x0, xr, ur, [])
+        np.testing.assert_allclose(s.optimal_control, so.optimal_control, atol=1e-9)
+        if i < 10:
+            assert abs(s.optimal_control[1]) <= 3.0 * (i + 1) / 10 + 1e-12
+    assert c._step_count == 12
+    c.reset()
+    assert c._step_count == 0
+
+
+def test_mpc_closed_loop_drop_in(rm):
+    """run_simulation.py --mode mpc loop (mpc_rate 5, 300 steps) with the HIP controller vs
+    the same loop on the exact-QP oracle."""
+    st_o, ct_o = sims.mpc_closed_loop(steps=300)
+    g = figure8.Figure8(2.0, 0.5, 0.02)
+    g.generate(20.0)
+    c = rm.MPCController(horizon=6, Q_diag=[15, 15, 50], R_diag=[.1, .1], P_diag=[30, 30, 40],
+                         d_safe=0.3, slack_penalty=5000.0, dt=0.02, v_max=2.0, omega_max=3.0,
+                         solver="OSQP", block_size=2)
+    obs = [rm.Obstacle(*o) for o in ompc.default_obstacles()]
+    x = g.reference_at_index(0)[0].copy()
+    cts = []
+    for k in range(300):
+        xr, ur = g.segment(k, 7)
+        if k % 5 == 0:
+            sol = c.solve_with_ltv(x, xr, ur, obs)
+        x = oplant.simulate_step(x, sol.optimal_control, 0.02, 2.0, 3.0)
+        cts.append(sol.optimal_control)
+    np.testing.assert_allclose(np.array(cts), ct_o, atol=1e-8, rtol=0)
+
+
+# ------------------------------------------------------------------------------------ misc
+def test_risk_matches_reference(rm, golden):
+    d = golden("risk.npz")
+    rmx = rm.RiskMetrics()
+    out, use, lvl = rmx.assess_risk_batch(d["states"], [tuple(o) for o in d["obstacles"]])
+    v = d["vals"]
+    np.testing.assert_allclose(out[:, 0], v[:, 0], atol=1e-12)
+    np.testing.assert_allclose(out[:, 2], v[:, 1], atol=1e-12)
+    np.testing.assert_allclose(out[:, 3], v[:, 2], atol=1e-12)
+    np.testing.assert_array_equal(out[:, 4], v[:, 3])
+    np.testing.assert_array_equal(use, v[:, 4].astype(bool))
+    outp, usep, _ = rmx.assess_risk_batch(d["states"], [tuple(o) for o in d["obstacles"]],
+                                          predicted_states=d["pred"])
+    np.testing.assert_allclose(outp[:, 1], v[:, 5], atol=1e-12)
+    np.testing.assert_allclose(outp[:, 2], v[:, 6], atol=1e-12)
+    np.testing.assert_array_equal(usep, v[:, 7].astype(bool))
+    a = rmx.assess_risk(d["states"][0], [dict(x=o[0], y=o[1], radius=o[2]) for o in d["obstacles"]])
+    assert a.risk_level in ("low", "medium", "high", "critical")
+
+
+def test_plant_matches_reference(rm, golden):
+    d = golden("plant.npz")
+    e = rm.batch.plant_step_batch(d["x"], d["u"], 0.02, 2.0, 3.0, "euler")
+    r = rm.batch.plant_step_batch(d["x"], d["u"], 0.02, 2.0, 3.0, "rk4")
+    np.testing.assert_allclose(e, d["euler"], atol=1e-14, rtol=0)
+    np.testing.assert_allclose(r, d["rk4"], atol=1e-14, rtol=0)
+
+
+def test_figure8_matches_reference(rm, golden):
+    d = golden("figure8.npz")
+    xr, ur = rm.batch.figure8_batch(np.zeros(1), 1000)
+    tab = d["table"]
+    np.testing.assert_allclose(xr[0], tab[:, 1:4], atol=1e-12, rtol=0)
+    np.testing.assert_allclose(ur[0], tab[:, 4:6], atol=1e-9, rtol=0)
+    xr, ur = rm.batch.figure8_batch(d["t_pts"], 1)
+    np.testing.assert_allclose(np.concatenate([xr[:, 0], ur[:, 0]], 1), d["at_time"], atol=1e-9)
+
+
+def test_hybrid_step_batch_matches_oracle_loop(rm):
+    """run_hybrid_simulation (run_simulation.py:413-576) for 3 robots over 150 steps on the
+    device (risk, dwell hysteresis, compaction, LQR/MPC branches) vs the oracle loop."""
+    steps, B = 150, 3
+    st_o, ct_o, used_o = sims.hybrid_closed_loop(steps=steps)
+    g = figure8.Figure8(2.0, 0.5, 0.02)
+    g.generate(20.0)
+    rp = rm._native.risk_params()
+    lp = rm._native.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0)
+    mp = rm._native.mpc_params(6, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                               0.02, block_size=1)
+    state = rm.batch.new_hybrid_state(B)
+    x = np.tile(g.reference_at_index(0)[0], (B, 1))
+    obs = ompc.default_obstacles()
+    for k in range(steps):
+        xs, us = g.segment(k, 7)
+        u, used, _ = rm.batch.hybrid_step_batch(rp, lp, mp, x, np.tile(xs, (B, 1, 1)),
+                                                np.tile(us, (B, 1, 1)), obs, state)
+        assert np.all(used == used_o[k]), k
+        np.testing.assert_allclose(u, np.tile(ct_o[k], (B, 1)), atol=1e-8, rtol=0)
+        x = rm.batch.plant_step_batch(x, u, 0.02, 2.0, 3.0)
+    np.testing.assert_allclose(x, np.tile(st_o[-1], (B, 1)), atol=1e-8)
