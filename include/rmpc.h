@@ -27,7 +27,9 @@
  *   - Functions without the _dev suffix take HOST pointers; the library stages them
  *     through device buffers it owns inside the context and returns after the results
  *     are back on the host (synchronous).  The _dev variants take DEVICE pointers and
- *     a hipStream_t (passed as void*; NULL = the context's stream) and are asynchronous.
+ *     a hipStream_t (passed as void*; NULL = the null stream, as in HIP) and are
+ *     asynchronous.  A context's scratch is shared by its _dev calls: issue them from one
+ *     stream at a time per context.
  *   - Return value: 0 on success, a negative RMPC_E* code on an API error (bad shape,
  *     null pointer, HIP failure).  rmpc_last_error() gives a thread-local message.
  *   - Numerical failure is never an API error: per robot, `status` says what happened

@@ -200,7 +200,9 @@ static hipError_t ensure_ws(RmpcCtx *c, const MpcLayout &L, int64_t B) {
     return c->ws.ensure(waves * (size_t)L.REC * RMPC_WAVE_LANES * sizeof(double));
 }
 
-static hipStream_t pick(RmpcCtx *c, void *s) { return s ? (hipStream_t)s : c->stream; }
+// _dev entry points run on the caller's stream; NULL is the null (default) stream, as in
+// HIP itself -- so torch's default stream (handle 0) works unchanged.
+static hipStream_t pick(RmpcCtx *, void *s) { return (hipStream_t)s; }
 
 // stage a host array to the device (returns device pointer or nullptr when src is null)
 template <typename T>

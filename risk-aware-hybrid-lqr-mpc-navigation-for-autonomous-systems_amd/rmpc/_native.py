@@ -100,6 +100,14 @@ def load():
             if not os.path.exists(LIB_PATH):
                 raise RmpcError(f"{LIB_PATH} not built: run __graft_entry__.build() "
                                 "(make -C <package dir>); there is no CPU fallback")
+            # One HIP runtime per process: PyTorch bundles its own libamdhip64.so.7 and its
+            # libraries NEED it by a different file name, so if librmpc.so were loaded first
+            # the process would end up with two runtimes (and torch's copy sees no device).
+            # Importing torch first makes librmpc.so bind to the runtime already loaded.
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
             lib = C.CDLL(LIB_PATH)
             for name, args in _PROTOS.items():
                 f = getattr(lib, name)
