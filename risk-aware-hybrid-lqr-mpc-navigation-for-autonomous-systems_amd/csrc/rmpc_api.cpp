@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -74,6 +75,7 @@ struct RmpcCtx {
     DevBuf ws;                 // solver workspace
     DevBuf stage[SB_COUNT];    // staging buffers for host-pointer entry points
     DevBuf idx_lqr, idx_mpc, counts, hyb_status;
+    DevBuf fast_gains, fast_usol, retry, retry_count;
     std::mutex mu;
 };
 
@@ -118,6 +120,10 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     c->idx_mpc.release();
     c->counts.release();
     c->hyb_status.release();
+    c->fast_gains.release();
+    c->fast_usol.release();
+    c->retry.release();
+    c->retry_count.release();
     (void)hipStreamDestroy(c->stream);
     delete c;
     return RMPC_OK;
@@ -204,6 +210,57 @@ static hipError_t ensure_ws(RmpcCtx *c, const MpcLayout &L, int64_t B) {
 // HIP itself -- so torch's default stream (handle 0) works unchanged.
 static hipStream_t pick(RmpcCtx *, void *s) { return (hipStream_t)s; }
 
+// Launch the MPC solve for B robots (or the robots of a device-side index list): the
+// register-resident kernel when (N, block size) is instantiated, followed by the generic
+// kernel on its retry list; otherwise the generic kernel alone.
+static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const double *x0,
+                      const double *x_refs, int32_t ref_rows, const double *u_refs, int32_t uref_rows,
+                      const double *obstacles, int32_t n_obs, int32_t *step_count, double *u0,
+                      double *u_seq, double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
+                      int32_t *iters, const int32_t *index, const int32_t *count, hipStream_t s) {
+    const int bs = p->formulation == RMPC_LTV ? p->block_size : 1;
+    const MpcLayout L = rmpc_mpc_layout(p->horizon, bs, n_obs);
+    HIP_TRY(ensure_ws(c, L, B));
+    const MpcDevParams d = to_dev(p);
+    const bool fast = p->formulation == RMPC_LTV && p->precision == RMPC_F64 &&
+                      rmpc_mpc_fast_supported(p->horizon, bs) && !getenv("RMPC_DISABLE_FAST");
+    if (!fast)
+        HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
+                                    step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
+                                    c->ws.p, index, count, s));
+    else {
+        const int nb = (p->horizon + bs - 1) / bs;
+        const size_t waves = (size_t)((B + RMPC_WAVE_LANES - 1) / RMPC_WAVE_LANES);
+        HIP_TRY(c->fast_gains.ensure(waves * nb * 4 * RMPC_WAVE_LANES * sizeof(double2)));
+        HIP_TRY(c->fast_usol.ensure(waves * nb * RMPC_WAVE_LANES * sizeof(double2)));
+        HIP_TRY(c->retry.ensure((size_t)B * sizeof(int32_t)));
+        HIP_TRY(c->retry_count.ensure(256));
+        HIP_TRY(hipMemsetAsync(c->retry_count.p, 0, 16, s));
+        MpcFastArgs a;
+        memset(&a, 0, sizeof(a));
+        a.prm = d;
+        a.B = B;
+        a.x0 = x0; a.x_refs = x_refs; a.u_refs = u_refs;
+        a.ref_rows = ref_rows; a.uref_rows = uref_rows; a.no = n_obs;
+        a.obs = obstacles;
+        a.step_count = step_count;
+        a.u0 = u0; a.u_seq = u_seq; a.x_pred = x_pred; a.cost = cost;
+        a.status = status; a.iters = iters; a.slack_used = slack_used;
+        a.gains = (double2 *)c->fast_gains.p;
+        a.usol = (double2 *)c->fast_usol.p;
+        a.index = index;
+        a.count = count;
+        a.retry = (int32_t *)c->retry.p;
+        a.retry_count = (int32_t *)c->retry_count.p;
+        HIP_TRY(rmpc_launch_mpc_fast_f64(a, p->horizon, bs, s));
+        HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
+                                    step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
+                                    c->ws.p, (const int32_t *)c->retry.p, (const int32_t *)c->retry_count.p,
+                                    s));
+    }
+    return RMPC_OK;
+}
+
 // stage a host array to the device (returns device pointer or nullptr when src is null)
 template <typename T>
 static int h2d(RmpcCtx *c, int slot, const T *src, size_t n, T **dst) {
@@ -249,14 +306,8 @@ extern "C" int rmpc_mpc_solve_batch_dev(RmpcCtx *c, const RmpcMpcParams *p, int6
     if (!x0 || !x_refs || !u_refs || !u0 || !status || (n_obs > 0 && !obstacles))
         return fail(RMPC_EINVAL, "required pointer is NULL");
     HIP_TRY(hipSetDevice(c->device));
-    const int bs = p->formulation == RMPC_LTV ? p->block_size : 1;
-    const MpcLayout L = rmpc_mpc_layout(p->horizon, bs, n_obs);
-    HIP_TRY(ensure_ws(c, L, B));
-    const MpcDevParams d = to_dev(p);
-    HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
-                                step_count, u0, u_seq, x_pred, cost, status, slack_used, iters, c->ws.p,
-                                nullptr, nullptr, pick(c, stream)));
-    return RMPC_OK;
+    return launch_mpc(c, p, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs, step_count, u0,
+                      u_seq, x_pred, cost, status, slack_used, iters, nullptr, nullptr, pick(c, stream));
 }
 
 extern "C" int rmpc_mpc_solve_batch(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const double *x0,
@@ -431,8 +482,6 @@ extern "C" int rmpc_hybrid_step_batch_dev(RmpcCtx *c, const RmpcRiskParams *rp, 
     HIP_TRY(c->idx_mpc.ensure((size_t)B * sizeof(int32_t)));
     HIP_TRY(c->counts.ensure(256));
     HIP_TRY(c->hyb_status.ensure((size_t)B * sizeof(int32_t)));
-    const MpcLayout L = rmpc_mpc_layout(mp->horizon, mp->block_size, n_obs);
-    HIP_TRY(ensure_ws(c, L, B));
     int32_t *cnt = (int32_t *)c->counts.p;
     HIP_TRY(hipMemsetAsync(cnt, 0, 16, s));
     HIP_TRY(rmpc_launch_hybrid_decide(to_dev(rp), B, x, obstacles, n_obs, prev_ctrl, steps_since, used_mpc,
@@ -442,11 +491,9 @@ extern "C" int rmpc_hybrid_step_batch_dev(RmpcCtx *c, const RmpcRiskParams *rp, 
                                     u_out, nullptr, nullptr, nullptr, nullptr, (const int32_t *)c->idx_lqr.p,
                                     cnt, s));
     // MPC branch: solve_with_ltv on the segment; writes u0 straight into u_out
-    HIP_TRY(rmpc_launch_mpc_f64(to_dev(mp), L, B, x, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
-                                step_count, u_out, nullptr, nullptr, nullptr,
-                                (int32_t *)c->hyb_status.p, nullptr, nullptr, c->ws.p,
-                                (const int32_t *)c->idx_mpc.p, cnt + 1, s));
-    return RMPC_OK;
+    return launch_mpc(c, mp, B, x, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs, step_count, u_out,
+                      nullptr, nullptr, nullptr, (int32_t *)c->hyb_status.p, nullptr, nullptr,
+                      (const int32_t *)c->idx_mpc.p, cnt + 1, s);
 }
 
 extern "C" int rmpc_hybrid_step_batch(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams *lp,

@@ -28,6 +28,25 @@ struct MpcLayout {
 
 MpcLayout rmpc_mpc_layout(int N, int bs, int no);
 
+// Arguments of the register-resident LTV kernel (rmpc_mpc_fast.hip).
+struct MpcFastArgs {
+    MpcDevParams prm;
+    int64_t B;                       // robots (or capacity of `index`)
+    const double *x0, *x_refs, *u_refs;
+    int ref_rows, uref_rows, no;
+    const double *obs;               // [no][3] (x, y, radius), device memory
+    int32_t *step_count;
+    double *u0, *u_seq, *x_pred, *cost;
+    int32_t *status, *iters;
+    uint8_t *slack_used;
+    double2 *gains, *usol;           // per-wave tiles
+    const int32_t *index, *count;    // optional robot index list (device-side length)
+    int32_t *retry, *retry_count;    // robots handed to the generic kernel
+};
+
+bool rmpc_mpc_fast_supported(int N, int bs);
+hipError_t rmpc_launch_mpc_fast_f64(const MpcFastArgs &a, int N, int bs, hipStream_t stream);
+
 hipError_t rmpc_launch_mpc_f64(const MpcDevParams &prm, const MpcLayout &L, int64_t B,
                                const double *x0, const double *x_refs, int ref_rows,
                                const double *u_refs, int uref_rows, const double *obstacles,

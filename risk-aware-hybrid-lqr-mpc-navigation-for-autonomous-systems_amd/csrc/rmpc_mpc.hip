@@ -17,6 +17,7 @@
 // load/store of a wave is a single coalesced 512-byte row.
 #include "rmpc_device.h"
 #include "rmpc_internal.h"
+#include "rmpc_riccati.h"
 
 namespace rmpc {
 
@@ -191,15 +192,13 @@ __device__ int riccati_pass(const MpcDevParams &p, const MpcLayout &L, const Wav
     const T Q0 = (T)p.Q[0], Q1 = (T)p.Q[1], Q2 = (T)p.Q[2];
     const T R0 = (T)p.R[0], R1 = (T)p.R[1];
     // V(x) = x'Px + 2p'x, terminal
-    T P00 = (T)p.P[0], P01 = 0, P02 = 0, P11 = (T)p.P[1], P12 = 0, P22 = (T)p.P[2];
-    T p0 = -(T)p.P[0] * w(L.XS0 + N), p1 = -(T)p.P[1] * w(L.XS1 + N), p2 = -(T)p.P[2] * w(L.XS2 + N);
+    RicV<T> V;
+    V.P00 = (T)p.P[0]; V.P01 = 0; V.P02 = 0; V.P11 = (T)p.P[1]; V.P12 = 0; V.P22 = (T)p.P[2];
+    V.p0 = -(T)p.P[0] * w(L.XS0 + N); V.p1 = -(T)p.P[1] * w(L.XS1 + N); V.p2 = -(T)p.P[2] * w(L.XS2 + N);
     for (int j = nb - 1; j >= 0; j--) {
         const int k0 = j * bs;
         const int k1 = min(k0 + bs, N);
-        T W00 = P00, W01 = P01, W02 = P02, W11 = P11, W12 = P12, W22 = P22;
-        T X00 = 0, X01 = 0, X10 = 0, X11 = 0, X20 = 0, X21 = 0;   // Wxu[i][c]
-        T U00 = 0, U01 = 0, U11 = 0;                               // Wuu
-        T wx0 = p0, wx1 = p1, wx2 = p2, wu0 = 0, wu1 = 0;
+        RicW<T> W = ric_open(V);
         for (int k = k1 - 1; k >= k0; k--) {
             T q00 = Q0, q01 = 0, q11 = Q1;
             T qv0 = -Q0 * w(L.XS0 + k), qv1 = -Q1 * w(L.XS1 + k), qv2 = -Q2 * w(L.XS2 + k);
@@ -216,95 +215,16 @@ __device__ int riccati_pass(const MpcDevParams &p, const MpcLayout &L, const Wav
                     }
                 }
             }
-            const T a0 = w(L.A0 + k), a1 = w(L.A1 + k), b0 = w(L.B0 + k), b1 = w(L.B1 + k);
-            // WB = Wxx B + Wxu
-            const T WB00 = W00 * b0 + W01 * b1 + X00, WB10 = W01 * b0 + W11 * b1 + X10,
-                    WB20 = W02 * b0 + W12 * b1 + X20;
-            const T WB01 = dt * W02 + X01, WB11 = dt * W12 + X11, WB21 = dt * W22 + X21;
-            // Wuu' = R + B'WB + Wxu'B + Wuu
-            const T nU00 = R0 + U00 + b0 * WB00 + b1 * WB10 + (X00 * b0 + X10 * b1);
-            const T nU01 = U01 + b0 * WB01 + b1 * WB11 + X20 * dt;
-            const T nU11 = R1 + U11 + dt * WB21 + X21 * dt;
-            // Wxu' = A' WB  (A' = I + e2 a')
-            const T nX00 = WB00, nX10 = WB10, nX20 = WB20 + a0 * WB00 + a1 * WB10;
-            const T nX01 = WB01, nX11 = WB11, nX21 = WB21 + a0 * WB01 + a1 * WB11;
-            // Wxx' = Qk + A'WA
-            const T v0 = W00 * a0 + W01 * a1, v1 = W01 * a0 + W11 * a1, v2 = W02 * a0 + W12 * a1;
-            const T aWa = a0 * v0 + a1 * v1;
-            const T nW00 = W00 + q00, nW01 = W01 + q01, nW11 = W11 + q11;
-            const T nW02 = W02 + v0, nW12 = W12 + v1, nW22 = W22 + (T)2 * v2 + aWa + Q2;
-            // linear terms
-            const T nwu0 = wu0 + R0 * w(L.US0 + k) + b0 * wx0 + b1 * wx1;
-            const T nwu1 = wu1 + R1 * w(L.US1 + k) + dt * wx2;
-            const T nwx2 = wx2 + a0 * wx0 + a1 * wx1 + qv2;
-            wx0 += qv0;
-            wx1 += qv1;
-            wx2 = nwx2;
-            wu0 = nwu0;
-            wu1 = nwu1;
-            W00 = nW00; W01 = nW01; W02 = nW02; W11 = nW11; W12 = nW12; W22 = nW22;
-            X00 = nX00; X10 = nX10; X20 = nX20; X01 = nX01; X11 = nX11; X21 = nX21;
-            U00 = nU00; U01 = nU01; U11 = nU11;
+            ric_step(W, w(L.A0 + k), w(L.A1 + k), w(L.B0 + k), w(L.B1 + k), dt, q00, q01, q11, Q2,
+                     qv0, qv1, qv2, R0, R1, R0 * w(L.US0 + k), R1 * w(L.US1 + k));
         }
-        // minimise u'Mu + 2u'(Lx + g) over the free components (M = Wuu, L = Wxu')
         const int bf0 = (int)w(L.BF0 + j), bf1 = (int)w(L.BF1 + j);
         const T uc0 = bf0 == 1 ? w(L.LO0 + j) : w(L.HI0 + j);
         const T uc1 = bf1 == 1 ? w(L.LO1 + j) : w(L.HI1 + j);
-        T K00, K01, K02, K10, K11, K12, k0v, k1v;
-        if (bf0 == 0 && bf1 == 0) {
-            const T id = (T)1 / (U00 * U11 - U01 * U01);
-            const T i00 = U11 * id, i01 = -U01 * id, i11 = U00 * id;
-            K00 = -(i00 * X00 + i01 * X01);
-            K01 = -(i00 * X10 + i01 * X11);
-            K02 = -(i00 * X20 + i01 * X21);
-            K10 = -(i01 * X00 + i11 * X01);
-            K11 = -(i01 * X10 + i11 * X11);
-            K12 = -(i01 * X20 + i11 * X21);
-            k0v = -(i00 * wu0 + i01 * wu1);
-            k1v = -(i01 * wu0 + i11 * wu1);
-        } else if (bf0 == 0) {
-            const T id = (T)1 / U00;
-            K00 = -X00 * id; K01 = -X10 * id; K02 = -X20 * id;
-            K10 = 0; K11 = 0; K12 = 0;
-            k0v = -(wu0 + U01 * uc1) * id;
-            k1v = uc1;
-        } else if (bf1 == 0) {
-            const T id = (T)1 / U11;
-            K10 = -X01 * id; K11 = -X11 * id; K12 = -X21 * id;
-            K00 = 0; K01 = 0; K02 = 0;
-            k1v = -(wu1 + U01 * uc0) * id;
-            k0v = uc0;
-        } else {
-            K00 = K01 = K02 = K10 = K11 = K12 = 0;
-            k0v = uc0;
-            k1v = uc1;
-        }
-        // MK = M K
-        const T MK00 = U00 * K00 + U01 * K10, MK01 = U00 * K01 + U01 * K11, MK02 = U00 * K02 + U01 * K12;
-        const T MK10 = U01 * K00 + U11 * K10, MK11 = U01 * K01 + U11 * K11, MK12 = U01 * K02 + U11 * K12;
-        const T Mk0 = U00 * k0v + U01 * k1v, Mk1 = U01 * k0v + U11 * k1v;
-        // store gains; for a fixed component the K row / k slot carry its multiplier map
-        // d(obj)/du_c = 2[(MK + L)_c x + (Mk + g)_c]
-        const int G = L.K;   // K fields: [0..5] x nb, kk [6..7] x nb
-        w(G + 0 * nb + j) = bf0 == 0 ? K00 : (T)2 * (MK00 + X00);
-        w(G + 1 * nb + j) = bf0 == 0 ? K01 : (T)2 * (MK01 + X10);
-        w(G + 2 * nb + j) = bf0 == 0 ? K02 : (T)2 * (MK02 + X20);
-        w(G + 3 * nb + j) = bf1 == 0 ? K10 : (T)2 * (MK10 + X01);
-        w(G + 4 * nb + j) = bf1 == 0 ? K11 : (T)2 * (MK11 + X11);
-        w(G + 5 * nb + j) = bf1 == 0 ? K12 : (T)2 * (MK12 + X21);
-        w(G + 6 * nb + j) = bf0 == 0 ? k0v : (T)2 * (Mk0 + wu0);
-        w(G + 7 * nb + j) = bf1 == 0 ? k1v : (T)2 * (Mk1 + wu1);
-        // value function: P = Wxx + K'MK + Wxu K + K'Wxu' ; p = wx + K'(Mk + g) + Wxu k
-        P00 = W00 + (K00 * MK00 + K10 * MK10) + (T)2 * (X00 * K00 + X01 * K10);
-        P11 = W11 + (K01 * MK01 + K11 * MK11) + (T)2 * (X10 * K01 + X11 * K11);
-        P22 = W22 + (K02 * MK02 + K12 * MK12) + (T)2 * (X20 * K02 + X21 * K12);
-        P01 = W01 + (K00 * MK01 + K10 * MK11) + (X00 * K01 + X01 * K11) + (K00 * X10 + K10 * X11);
-        P02 = W02 + (K00 * MK02 + K10 * MK12) + (X00 * K02 + X01 * K12) + (K00 * X20 + K10 * X21);
-        P12 = W12 + (K01 * MK02 + K11 * MK12) + (X10 * K02 + X11 * K12) + (K01 * X20 + K11 * X21);
-        const T g0 = Mk0 + wu0, g1 = Mk1 + wu1;
-        p0 = wx0 + K00 * g0 + K10 * g1 + X00 * k0v + X01 * k1v;
-        p1 = wx1 + K01 * g0 + K11 * g1 + X10 * k0v + X11 * k1v;
-        p2 = wx2 + K02 * g0 + K12 * g1 + X20 * k0v + X21 * k1v;
+        T G[8];
+        V = ric_block(W, bf0, bf1, uc0, uc1, G);
+#pragma unroll
+        for (int i = 0; i < 8; i++) w(L.K + i * nb + j) = G[i];
     }
     // ---- forward pass + set update
     const T eps_h = (T)1e-14, eps_b = (T)1e-13;
@@ -322,13 +242,7 @@ __device__ int riccati_pass(const MpcDevParams &p, const MpcLayout &L, const Wav
         const T u0v = bf0 == 0 ? e0 : (bf0 == 1 ? lo0 : hi0);
         const T u1v = bf1 == 0 ? e1 : (bf1 == 1 ? lo1 : hi1);
         // box set update (lambda = e when fixed)
-        int ns0 = bf0, ns1 = bf1;
-        if (bf0 == 0) { if (u0v < lo0 - eps_b) ns0 = 1; else if (u0v > hi0 + eps_b) ns0 = 2; }
-        else if (bf0 == 1) { if (e0 < 0) ns0 = 0; }
-        else { if (e0 > 0) ns0 = 0; }
-        if (bf1 == 0) { if (u1v < lo1 - eps_b) ns1 = 1; else if (u1v > hi1 + eps_b) ns1 = 2; }
-        else if (bf1 == 1) { if (e1 < 0) ns1 = 0; }
-        else { if (e1 > 0) ns1 = 0; }
+        const int ns0 = box_rule(bf0, e0, lo0, hi0, eps_b), ns1 = box_rule(bf1, e1, lo1, hi1, eps_b);
         if (ns0 != bf0 || ns1 != bf1) {
             changed = 1;
             if (mode == 0) { w(L.BF0 + j) = (T)ns0; w(L.BF1 + j) = (T)ns1; }

@@ -1,0 +1,180 @@
+// rmpc_riccati.h -- the per-robot algebra of the MPC solve, shared by the generic
+// (workspace) kernel and the register-resident fast kernel so both do bit-identical
+// arithmetic.
+//
+// Problem (one robot, slack eliminated):
+//   min  sum_k (x_k - xs_k)'Q(x_k - xs_k) + (u_b(k) + us_k)'R(u_b(k) + us_k)
+//        + (x_N - xs_N)'P(x_N - xs_N) + rho * sum_rows max(0, hb - n . pos(x_k))^2
+//   s.t. x_{k+1} = A_k x_k + B_k u_b(k),  lo_b <= u_b <= hi_b
+// with A_k = I + (a0, a1, 0) e_theta', B_k = [[b0, 0], [b1, 0], [0, dt]] (the explicit
+// Euler linearisation of linearization.py:190-225).
+#pragma once
+#include "rmpc_device.h"
+
+namespace rmpc {
+
+// Within-block backward accumulator: W(x, u) = [x;u]'[[Wxx, Wxu],[Wxu', Wuu]][x;u] + 2[wx;wu]'[x;u]
+template <typename T>
+struct RicW {
+    T W00, W01, W02, W11, W12, W22;   // Wxx (sym)
+    T X00, X10, X20, X01, X11, X21;   // Wxu[i][c]
+    T U00, U01, U11;                  // Wuu (sym)
+    T wx0, wx1, wx2, wu0, wu1;
+};
+
+// Value function V(x) = x'Px + 2p'x
+template <typename T>
+struct RicV {
+    T P00, P01, P02, P11, P12, P22, p0, p1, p2;
+};
+
+template <typename T>
+__device__ __forceinline__ RicW<T> ric_open(const RicV<T> &v) {
+    RicW<T> w;
+    w.W00 = v.P00; w.W01 = v.P01; w.W02 = v.P02; w.W11 = v.P11; w.W12 = v.P12; w.W22 = v.P22;
+    w.X00 = 0; w.X10 = 0; w.X20 = 0; w.X01 = 0; w.X11 = 0; w.X21 = 0;
+    w.U00 = 0; w.U01 = 0; w.U11 = 0;
+    w.wx0 = v.p0; w.wx1 = v.p1; w.wx2 = v.p2; w.wu0 = 0; w.wu1 = 0;
+    return w;
+}
+
+// One backward step inside a block: W <- stage_k + W(A_k x + B_k u, u).
+// Stage k: state cost Q (diag, plus the pos block q00/q01/q11 of active hinge rows and
+// Q2), linear qv, input R and linear r (= R * us_k).
+template <typename T>
+__device__ __forceinline__ void ric_step(RicW<T> &s, T a0, T a1, T b0, T b1, T dt, T q00, T q01,
+                                         T q11, T Q2, T qv0, T qv1, T qv2, T R0, T R1, T r0,
+                                         T r1) {
+    const T WB00 = s.W00 * b0 + s.W01 * b1 + s.X00, WB10 = s.W01 * b0 + s.W11 * b1 + s.X10,
+            WB20 = s.W02 * b0 + s.W12 * b1 + s.X20;
+    const T WB01 = dt * s.W02 + s.X01, WB11 = dt * s.W12 + s.X11, WB21 = dt * s.W22 + s.X21;
+    const T nU00 = R0 + s.U00 + b0 * WB00 + b1 * WB10 + (s.X00 * b0 + s.X10 * b1);
+    const T nU01 = s.U01 + b0 * WB01 + b1 * WB11 + s.X20 * dt;
+    const T nU11 = R1 + s.U11 + dt * WB21 + s.X21 * dt;
+    const T nX20 = WB20 + a0 * WB00 + a1 * WB10;
+    const T nX21 = WB21 + a0 * WB01 + a1 * WB11;
+    const T v0 = s.W00 * a0 + s.W01 * a1, v1 = s.W01 * a0 + s.W11 * a1, v2 = s.W02 * a0 + s.W12 * a1;
+    const T aWa = a0 * v0 + a1 * v1;
+    const T nW22 = s.W22 + (T)2 * v2 + aWa + Q2;
+    const T nwu0 = s.wu0 + r0 + b0 * s.wx0 + b1 * s.wx1;
+    const T nwu1 = s.wu1 + r1 + dt * s.wx2;
+    const T nwx2 = s.wx2 + a0 * s.wx0 + a1 * s.wx1 + qv2;
+    s.wx0 += qv0;
+    s.wx1 += qv1;
+    s.wx2 = nwx2;
+    s.wu0 = nwu0;
+    s.wu1 = nwu1;
+    s.W02 = s.W02 + v0;
+    s.W12 = s.W12 + v1;
+    s.W00 = s.W00 + q00;
+    s.W01 = s.W01 + q01;
+    s.W11 = s.W11 + q11;
+    s.W22 = nW22;
+    s.X00 = WB00; s.X10 = WB10; s.X20 = nX20; s.X01 = WB01; s.X11 = WB11; s.X21 = nX21;
+    s.U00 = nU00; s.U01 = nU01; s.U11 = nU11;
+}
+
+// Gains of one block: minimise u'Mu + 2u'(Lx + g) over the free components (M = Wuu,
+// L = Wxu', g = wu); bf = 0 free, 1 at lower (value uc), 2 at upper.  G[0..5] = K rows,
+// G[6..7] = k.  For a FIXED component the K row / k slot hold its multiplier map
+// d(obj)/du_c = 2[(MK + L)_c x + (Mk + g)_c] instead (K_c = 0, k_c = uc implied).
+// Returns the value function of the block start.
+template <typename T>
+__device__ __forceinline__ RicV<T> ric_block(const RicW<T> &s, int bf0, int bf1, T uc0, T uc1,
+                                             T G[8]) {
+    T K00, K01, K02, K10, K11, K12, k0v, k1v;
+    if (bf0 == 0 && bf1 == 0) {
+        const T id = (T)1 / (s.U00 * s.U11 - s.U01 * s.U01);
+        const T i00 = s.U11 * id, i01 = -s.U01 * id, i11 = s.U00 * id;
+        K00 = -(i00 * s.X00 + i01 * s.X01);
+        K01 = -(i00 * s.X10 + i01 * s.X11);
+        K02 = -(i00 * s.X20 + i01 * s.X21);
+        K10 = -(i01 * s.X00 + i11 * s.X01);
+        K11 = -(i01 * s.X10 + i11 * s.X11);
+        K12 = -(i01 * s.X20 + i11 * s.X21);
+        k0v = -(i00 * s.wu0 + i01 * s.wu1);
+        k1v = -(i01 * s.wu0 + i11 * s.wu1);
+    } else if (bf0 == 0) {
+        const T id = (T)1 / s.U00;
+        K00 = -s.X00 * id; K01 = -s.X10 * id; K02 = -s.X20 * id;
+        K10 = 0; K11 = 0; K12 = 0;
+        k0v = -(s.wu0 + s.U01 * uc1) * id;
+        k1v = uc1;
+    } else if (bf1 == 0) {
+        const T id = (T)1 / s.U11;
+        K10 = -s.X01 * id; K11 = -s.X11 * id; K12 = -s.X21 * id;
+        K00 = 0; K01 = 0; K02 = 0;
+        k1v = -(s.wu1 + s.U01 * uc0) * id;
+        k0v = uc0;
+    } else {
+        K00 = K01 = K02 = K10 = K11 = K12 = 0;
+        k0v = uc0;
+        k1v = uc1;
+    }
+    const T MK00 = s.U00 * K00 + s.U01 * K10, MK01 = s.U00 * K01 + s.U01 * K11,
+            MK02 = s.U00 * K02 + s.U01 * K12;
+    const T MK10 = s.U01 * K00 + s.U11 * K10, MK11 = s.U01 * K01 + s.U11 * K11,
+            MK12 = s.U01 * K02 + s.U11 * K12;
+    const T Mk0 = s.U00 * k0v + s.U01 * k1v, Mk1 = s.U01 * k0v + s.U11 * k1v;
+    G[0] = bf0 == 0 ? K00 : (T)2 * (MK00 + s.X00);
+    G[1] = bf0 == 0 ? K01 : (T)2 * (MK01 + s.X10);
+    G[2] = bf0 == 0 ? K02 : (T)2 * (MK02 + s.X20);
+    G[3] = bf1 == 0 ? K10 : (T)2 * (MK10 + s.X01);
+    G[4] = bf1 == 0 ? K11 : (T)2 * (MK11 + s.X11);
+    G[5] = bf1 == 0 ? K12 : (T)2 * (MK12 + s.X21);
+    G[6] = bf0 == 0 ? k0v : (T)2 * (Mk0 + s.wu0);
+    G[7] = bf1 == 0 ? k1v : (T)2 * (Mk1 + s.wu1);
+    RicV<T> v;
+    v.P00 = s.W00 + (K00 * MK00 + K10 * MK10) + (T)2 * (s.X00 * K00 + s.X01 * K10);
+    v.P11 = s.W11 + (K01 * MK01 + K11 * MK11) + (T)2 * (s.X10 * K01 + s.X11 * K11);
+    v.P22 = s.W22 + (K02 * MK02 + K12 * MK12) + (T)2 * (s.X20 * K02 + s.X21 * K12);
+    v.P01 = s.W01 + (K00 * MK01 + K10 * MK11) + (s.X00 * K01 + s.X01 * K11) + (K00 * s.X10 + K10 * s.X11);
+    v.P02 = s.W02 + (K00 * MK02 + K10 * MK12) + (s.X00 * K02 + s.X01 * K12) + (K00 * s.X20 + K10 * s.X21);
+    v.P12 = s.W12 + (K01 * MK02 + K11 * MK12) + (s.X10 * K02 + s.X11 * K12) + (K01 * s.X20 + K11 * s.X21);
+    const T g0 = Mk0 + s.wu0, g1 = Mk1 + s.wu1;
+    v.p0 = s.wx0 + K00 * g0 + K10 * g1 + s.X00 * k0v + s.X01 * k1v;
+    v.p1 = s.wx1 + K01 * g0 + K11 * g1 + s.X10 * k0v + s.X11 * k1v;
+    v.p2 = s.wx2 + K02 * g0 + K12 * g1 + s.X20 * k0v + s.X21 * k1v;
+    return v;
+}
+
+// Forward: u (or, for fixed components, the bound) and multiplier e at state x; applies
+// the PDAS box rule.  Returns the new box state for component c.
+template <typename T>
+__device__ __forceinline__ int box_rule(int bf, T e, T lo, T hi, T eps_b) {
+    int ns = bf;
+    if (bf == 0) {
+        if (e < lo - eps_b) ns = 1;
+        else if (e > hi + eps_b) ns = 2;
+    } else if (bf == 1) {
+        if (e < 0) ns = 0;
+    } else {
+        if (e > 0) ns = 0;
+    }
+    return ns;
+}
+
+// Linearised obstacle half-space of mpc_controller.py:439-468 (LTV: rows on dx with the
+// reference point p) -- kept when soft and dist > 0.01; r = hb - n . dp.
+__device__ __forceinline__ bool hinge_row_ltv(double px, double py, double ox, double oy, double safe,
+                                              double &n0, double &n1, double &hb) {
+    const double ddx = px - ox, ddy = py - oy;
+    const double dist = sqrt(ddx * ddx + ddy * ddy);
+    if (!(dist > 0.01)) return false;
+    n0 = ddx / dist;
+    n1 = ddy / dist;
+    hb = safe - (n0 * (px - ox) + n1 * (py - oy));
+    return true;
+}
+
+// np.unwrap step (numpy 2.x): correction increment for consecutive samples prev -> th
+__device__ __forceinline__ double unwrap_step(double prev, double th) {
+    const double dd = th - prev;
+    double ddmod = np_mod(dd + RMPC_PI, 2.0 * RMPC_PI) - RMPC_PI;
+    if (ddmod == -RMPC_PI && dd > 0) ddmod = RMPC_PI;
+    double ph = ddmod - dd;
+    if (fabs(dd) < RMPC_PI) ph = 0.0;
+    return ph;
+}
+
+}  // namespace rmpc
