@@ -253,10 +253,11 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         a.retry = (int32_t *)c->retry.p;
         a.retry_count = (int32_t *)c->retry_count.p;
         HIP_TRY(rmpc_launch_mpc_fast_f64(a, p->horizon, bs, s));
+        // retries are few (PDAS cycling / non-finite data): LDS-resident generic kernel
         HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
                                     step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
                                     c->ws.p, (const int32_t *)c->retry.p, (const int32_t *)c->retry_count.p,
-                                    s));
+                                    s, rmpc_mpc_lds_lanes(L)));
     }
     return RMPC_OK;
 }

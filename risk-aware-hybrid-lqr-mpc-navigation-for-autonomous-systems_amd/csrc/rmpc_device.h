@@ -35,13 +35,15 @@ __device__ __forceinline__ T clampv(T v, T lo, T hi) {
     return v < lo ? lo : (v > hi ? hi : v);
 }
 
-// Per-wave workspace tile: robot record field f, element i of the lane lives at
-// tile[(f + i) * 64 + lane] -- every access of a wave is one coalesced 512-B (f64) row.
+// Per-robot workspace record, lane-interleaved: element `off` of the lane lives at
+// base[off * stride + lane].  Global tiles use stride 64 (one coalesced 512-B row per wave
+// access); LDS tiles use the workgroup width (lane-contiguous, conflict-free ds_read_b64).
 template <typename T>
 struct WaveTile {
     T *base;
     int lane;
-    __device__ __forceinline__ T &operator()(int off) const { return base[(size_t)off * RMPC_WAVE + lane]; }
+    int stride;
+    __device__ __forceinline__ T &operator()(int off) const { return base[(size_t)off * stride + lane]; }
 };
 
 }  // namespace rmpc

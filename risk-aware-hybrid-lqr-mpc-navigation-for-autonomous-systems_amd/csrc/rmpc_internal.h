@@ -5,7 +5,7 @@
 
 #include "../../include/rmpc.h"
 
-#define RMPC_PDAS_ITERS 8
+#define RMPC_PDAS_ITERS 32   // PDAS solves before the projected-Newton phase
 #define RMPC_WAVE_LANES 64
 
 // Flattened, kernel-argument form of RmpcMpcParams.
@@ -53,7 +53,9 @@ hipError_t rmpc_launch_mpc_f64(const MpcDevParams &prm, const MpcLayout &L, int6
                                int n_obs, int32_t *step_count, double *u0, double *u_seq,
                                double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
                                int32_t *iters, void *ws, const int32_t *index,
-                               const int32_t *count, hipStream_t stream);
+                               const int32_t *count, hipStream_t stream, int lds_lanes = 0);
+// lanes per workgroup for the LDS-resident generic kernel (0 = record too large for LDS)
+int rmpc_mpc_lds_lanes(const MpcLayout &L);
 
 struct LqrDevParams {
     double Q[3], R[2];

@@ -367,7 +367,24 @@ __device__ void gradient(const MpcDevParams &p, const MpcLayout &L, const WaveTi
     }
 }
 
+// signature of the active sets (PDAS cycle detection; same hash as the fast kernel)
 template <typename T>
+__device__ uint64_t set_signature(const MpcLayout &L, const WaveTile<T> &w) {
+    uint64_t h = 1469598103934665603ull;
+    for (int k = 0; k < L.N; k++) {
+        uint32_t word = 0;
+        for (int o = 0; o < L.no; o++) word |= (uint32_t)(w(L.HACT + k * L.no + o) != (T)0) << o;
+        h = (h ^ (uint64_t)word) * 1099511628211ull;
+    }
+    for (int j = 0; j < L.nb; j++)
+        h = (h ^ (uint64_t)((int)w(L.BF0 + j) | ((int)w(L.BF1 + j) << 2))) * 1099511628211ull;
+    return h;
+}
+
+// USE_LDS: the whole robot record lives in LDS (workgroup = blockDim lanes, sized by the
+// host so the records fit in 160 KiB) -- used for the small retry lists, where latency
+// per robot, not occupancy, decides the launch time.
+template <typename T, bool USE_LDS>
 __global__ __launch_bounds__(256) void mpc_solve_kernel(MpcArgs<T> a) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t nrob = a.index ? (int64_t)*a.count : a.B;
@@ -375,7 +392,11 @@ __global__ __launch_bounds__(256) void mpc_solve_kernel(MpcArgs<T> a) {
     const int64_t b = a.index ? (int64_t)a.index[t] : t;
     const MpcLayout &L = a.L;
     const MpcDevParams &p = a.prm;
-    WaveTile<T> w{a.ws + (size_t)(t / RMPC_WAVE) * (size_t)L.REC * RMPC_WAVE, (int)(t % RMPC_WAVE)};
+    extern __shared__ double lds_ws[];
+    WaveTile<T> w = USE_LDS
+        ? WaveTile<T>{(T *)lds_ws, (int)threadIdx.x, (int)blockDim.x}
+        : WaveTile<T>{a.ws + (size_t)(t / RMPC_WAVE) * (size_t)L.REC * RMPC_WAVE, (int)(t % RMPC_WAVE),
+                      RMPC_WAVE};
     const int ltv = p.ltv;
     T x0[3];
     if (ltv) setup_ltv(a, w, b, x0);
@@ -387,10 +408,14 @@ __global__ __launch_bounds__(256) void mpc_solve_kernel(MpcArgs<T> a) {
     int cert = 0, it = 0;
     const int max_iter = p.max_iter;
     if (finite) {
-        // ---- phase 1: primal-dual active set
+        // ---- phase 1: primal-dual active set (capped; a repeated signature = cycling)
+        uint64_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
         for (; it < max_iter && it < RMPC_PDAS_ITERS;) {
             it++;
             if (!riccati_pass(p, L, w, x0, 0)) { cert = 1; break; }
+            const uint64_t sig = set_signature(L, w);
+            if (sig == h0 || sig == h1 || sig == h2 || sig == h3) break;
+            h3 = h2; h2 = h1; h1 = h0; h0 = sig;
         }
         if (!cert && it < max_iter) {
             // ---- phase 2: projected Newton + Armijo from the projected last iterate
@@ -561,13 +586,21 @@ MpcLayout rmpc_mpc_layout(int N, int bs, int no) {
     return L;
 }
 
+int rmpc_mpc_lds_lanes(const MpcLayout &L) {
+    const size_t per_lane = (size_t)L.REC * sizeof(double);
+    const size_t cap = 160 * 1024;
+    int lanes = 64;
+    while (lanes > 0 && (size_t)lanes * per_lane > cap) lanes >>= 1;
+    return lanes;
+}
+
 hipError_t rmpc_launch_mpc_f64(const MpcDevParams &prm, const MpcLayout &L, int64_t B,
                                const double *x0, const double *x_refs, int ref_rows,
                                const double *u_refs, int uref_rows, const double *obstacles,
                                int n_obs, int32_t *step_count, double *u0, double *u_seq,
                                double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
                                int32_t *iters, void *ws, const int32_t *index,
-                               const int32_t *count, hipStream_t stream) {
+                               const int32_t *count, hipStream_t stream, int lds_lanes) {
     MpcArgs<double> a;
     a.prm = prm;
     a.L = L;
@@ -581,8 +614,23 @@ hipError_t rmpc_launch_mpc_f64(const MpcDevParams &prm, const MpcLayout &L, int6
     a.index = index;
     a.count = count;
     if (B <= 0) return hipSuccess;
-    const int threads = 256;
-    const int64_t blocks = (B + threads - 1) / threads;
-    hipLaunchKernelGGL(mpc_solve_kernel<double>, dim3((unsigned)blocks), dim3(threads), 0, stream, a);
+    if (lds_lanes > 0) {
+        const size_t lds = (size_t)L.REC * lds_lanes * sizeof(double);
+        static bool attr_set = false;
+        if (!attr_set) {
+            hipError_t e = hipFuncSetAttribute((const void *)mpc_solve_kernel<double, true>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (e != hipSuccess) return e;
+            attr_set = true;
+        }
+        const int64_t blocks = (B + lds_lanes - 1) / lds_lanes;
+        hipLaunchKernelGGL((mpc_solve_kernel<double, true>), dim3((unsigned)blocks), dim3(lds_lanes), lds,
+                           stream, a);
+    } else {
+        const int threads = 256;
+        const int64_t blocks = (B + threads - 1) / threads;
+        hipLaunchKernelGGL((mpc_solve_kernel<double, false>), dim3((unsigned)blocks), dim3(threads), 0,
+                           stream, a);
+    }
     return hipGetLastError();
 }

@@ -77,6 +77,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     int it = 0, cert = 0, used = 0;
     double J = 0.0;
     const int maxit = min(p.max_iter, RMPC_PDAS_ITERS);
+    uint64_t hist0 = 0, hist1 = 0, hist2 = 0, hist3 = 0;   // active-set signatures (cycles)
     while (fin && it < maxit) {
         it++;
         // Keep the per-step inputs opaque to the optimiser at every iteration: otherwise it
@@ -210,6 +211,15 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         }
         J += p.P[0] * x0 * x0 + p.P[1] * x1 * x1 + p.P[2] * x2 * x2;
         if (!changed) { cert = 1; break; }
+        // PDAS cycling: a repeated active-set signature hands the robot to the
+        // projected-Newton phase of the generic kernel
+        uint64_t sig = 1469598103934665603ull;
+#pragma unroll
+        for (int k = 0; k < N; k++) sig = (sig ^ (uint64_t)Hf[k]) * 1099511628211ull;
+#pragma unroll
+        for (int j = 0; j < NB; j++) sig = (sig ^ (uint64_t)Bf[j]) * 1099511628211ull;
+        if (sig == hist0 || sig == hist1 || sig == hist2 || sig == hist3) break;
+        hist3 = hist2; hist2 = hist1; hist1 = hist0; hist0 = sig;
     }
     if (!cert || !isfinite(J)) {
         a.retry[atomicAdd(a.retry_count, 1)] = (int32_t)b;    // generic kernel takes over
