@@ -367,6 +367,10 @@ static uint64_t set_signature(const Prob *pr, const uint8_t hact[NM][OM], const 
  *          from the projected last iterate, with the same Riccati solve as its Newton step;
  *          it certifies with the same set-reproduction test.                           */
 #define PDAS_ITERS 32
+static long g_cnt[4];
+           /* diagnostics: phase-2 entries, phase-2 iterations, F evaluations */
+long rmpc_cpu_counter(int i) { return (i >= 0 && i < 4) ? g_cnt[i] : 0; }
+void rmpc_cpu_reset_counters(void) { memset(g_cnt, 0, sizeof(g_cnt)); }
 static int pdas_solve(const Prob *pr, int max_iter, Sol *s) {
     uint8_t hact[NM][OM];
     uint8_t bfix[NM][2];
@@ -395,6 +399,7 @@ static int pdas_solve(const Prob *pr, int max_iter, Sol *s) {
         return 0;
     }
     /* ---- phase 2: globalised projected Newton from the projected last iterate */
+    g_cnt[0]++;
     double z[NM][2], g[NM][2], x[NM + 1][3];
     for (int j = 0; j < pr->nb; j++)
         for (int c = 0; c < 2; c++) z[j][c] = clampd(s->u[j][c], pr->lo[j][c], pr->hi[j][c]);
@@ -420,6 +425,7 @@ static int pdas_solve(const Prob *pr, int max_iter, Sol *s) {
             }
         riccati_solve(pr, (const uint8_t(*)[OM])hact, (const uint8_t(*)[2])bfix, s, lam);
         s->iters = ++it;
+        g_cnt[1]++;
         uint8_t h2[NM][OM], b2[NM][2];
         memcpy(h2, hact, sizeof(h2));
         memcpy(b2, bfix, sizeof(b2));
@@ -438,6 +444,7 @@ static int pdas_solve(const Prob *pr, int max_iter, Sol *s) {
                     gd += g[j][c] * (zt[j][c] - z[j][c]);
                 }
             Ft = simulate_F(pr, (const double(*)[2])zt, xt);
+            g_cnt[2]++;
             if (Ft <= F + 1e-4 * gd) { acc = 1; break; }
             alpha *= 0.5;
         }

@@ -252,6 +252,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         a.count = count;
         a.retry = (int32_t *)c->retry.p;
         a.retry_count = (int32_t *)c->retry_count.p;
+        a.pdas_cap = getenv("RMPC_FAST_CAP") ? atoi(getenv("RMPC_FAST_CAP")) : 8;
         HIP_TRY(rmpc_launch_mpc_fast_f64(a, p->horizon, bs, s));
         // retries are few (PDAS cycling / non-finite data): LDS-resident generic kernel
         HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,

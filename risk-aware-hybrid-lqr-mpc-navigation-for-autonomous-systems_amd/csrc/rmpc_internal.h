@@ -42,6 +42,7 @@ struct MpcFastArgs {
     double2 *gains, *usol;           // per-wave tiles
     const int32_t *index, *count;    // optional robot index list (device-side length)
     int32_t *retry, *retry_count;    // robots handed to the generic kernel
+    int pdas_cap;                    // PDAS solves before a robot is handed on
 };
 
 bool rmpc_mpc_fast_supported(int N, int bs);

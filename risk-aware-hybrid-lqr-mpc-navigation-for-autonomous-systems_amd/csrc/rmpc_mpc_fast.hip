@@ -76,7 +76,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
 
     int it = 0, cert = 0, used = 0;
     double J = 0.0;
-    const int maxit = min(p.max_iter, RMPC_PDAS_ITERS);
+    const int maxit = min(p.max_iter, a.pdas_cap);
     uint64_t hist0 = 0, hist1 = 0, hist2 = 0, hist3 = 0;   // active-set signatures (cycles)
     while (fin && it < maxit) {
         it++;

@@ -24,4 +24,5 @@ def assert_gains_match(grid, K, P, K_ref, P_ref, Q, R):
         assert d <= tol, (v, t, d, tol)
         rs = dare_residual(P[i], v, t, Q, R)
         rr = dare_residual(P_ref[i], v, t, Q, R)
-        assert rs <= max(4 * rr, 1e-13), (v, t, rs, rr)   # both at rounding level
+        floor = 1e-13 if abs(v) >= 0.1 else 1e-12    # ||P|| up to 5e5 below v_r = 0.01
+        assert rs <= max(4 * rr, floor), (v, t, rs, rr)   # both at rounding level
