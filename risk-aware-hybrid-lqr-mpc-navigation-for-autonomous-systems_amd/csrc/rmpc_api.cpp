@@ -75,7 +75,7 @@ struct RmpcCtx {
     DevBuf ws;                 // solver workspace
     DevBuf stage[SB_COUNT];    // staging buffers for host-pointer entry points
     DevBuf idx_lqr, idx_mpc, counts, hyb_status;
-    DevBuf fast_gains, fast_usol, retry, retry_count;
+    DevBuf fast_gains, fast_usol, retry, retry2, retry_count, prof;
     std::mutex mu;
 };
 
@@ -123,6 +123,8 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     c->fast_gains.release();
     c->fast_usol.release();
     c->retry.release();
+    c->retry2.release();
+    c->prof.release();
     c->retry_count.release();
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -210,9 +212,19 @@ static hipError_t ensure_ws(RmpcCtx *c, const MpcLayout &L, int64_t B) {
 // HIP itself -- so torch's default stream (handle 0) works unchanged.
 static hipStream_t pick(RmpcCtx *, void *s) { return (hipStream_t)s; }
 
+// RMPC_DEBUG_SYNC=1: synchronise after each kernel of a solve and report (diagnostics)
+static void dbg_sync(hipStream_t s, const char *what) {
+    static const bool on = getenv("RMPC_DEBUG_SYNC") != nullptr;
+    if (!on) return;
+    const hipError_t e = hipStreamSynchronize(s);
+    fprintf(stderr, "[rmpc] %s done: %s\n", what, hipGetErrorString(e));
+}
+
 // Launch the MPC solve for B robots (or the robots of a device-side index list): the
-// register-resident kernel when (N, block size) is instantiated, followed by the generic
-// kernel on its retry list; otherwise the generic kernel alone.
+// register-resident lane-per-robot kernel when (N, block size) is instantiated; the robots
+// it does not certify within its PDAS cap go to the wave-per-robot dense kernel, and what
+// that one hands on (non-finite data -> fallback law, uncertified) to the generic kernel.
+// Otherwise the generic kernel alone.
 static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const double *x0,
                       const double *x_refs, int32_t ref_rows, const double *u_refs, int32_t uref_rows,
                       const double *obstacles, int32_t n_obs, int32_t *step_count, double *u0,
@@ -235,7 +247,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         HIP_TRY(c->fast_usol.ensure(waves * nb * RMPC_WAVE_LANES * sizeof(double2)));
         HIP_TRY(c->retry.ensure((size_t)B * sizeof(int32_t)));
         HIP_TRY(c->retry_count.ensure(256));
-        HIP_TRY(hipMemsetAsync(c->retry_count.p, 0, 16, s));
+        HIP_TRY(hipMemsetAsync(c->retry_count.p, 0, 64, s));
         MpcFastArgs a;
         memset(&a, 0, sizeof(a));
         a.prm = d;
@@ -252,13 +264,53 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         a.count = count;
         a.retry = (int32_t *)c->retry.p;
         a.retry_count = (int32_t *)c->retry_count.p;
-        a.pdas_cap = getenv("RMPC_FAST_CAP") ? atoi(getenv("RMPC_FAST_CAP")) : 8;
+        a.pdas_cap = getenv("RMPC_FAST_CAP") ? atoi(getenv("RMPC_FAST_CAP")) : 10;
         HIP_TRY(rmpc_launch_mpc_fast_f64(a, p->horizon, bs, s));
-        // retries are few (PDAS cycling / non-finite data): LDS-resident generic kernel
+        dbg_sync(s, "fast");
+        const int32_t *left = (const int32_t *)c->retry.p;
+        const int32_t *left_n = (const int32_t *)c->retry_count.p;
+        if (rmpc_mpc_dense_supported(p->horizon, bs, n_obs) && !getenv("RMPC_DISABLE_DENSE")) {
+            HIP_TRY(c->retry2.ensure((size_t)B * sizeof(int32_t)));
+            int32_t *cnt2 = (int32_t *)c->retry_count.p + 8;
+            // RMPC_DENSE_PROF=1: per-phase cycle counters of the dense kernel to stderr
+            // (synchronises the stream; diagnostics only)
+            const bool prof = getenv("RMPC_DENSE_PROF") != nullptr;
+            unsigned long long *pc = nullptr;
+            if (prof) {
+                HIP_TRY(c->prof.ensure(64 * sizeof(unsigned long long)));
+                pc = (unsigned long long *)c->prof.p;
+                HIP_TRY(hipMemsetAsync(pc, 0, 64 * sizeof(unsigned long long), s));
+            }
+            HIP_TRY(rmpc_launch_mpc_dense_f64(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs,
+                                              uref_rows, obstacles, step_count, u0, u_seq, x_pred, cost,
+                                              status, slack_used, iters, left, left_n,
+                                              (int32_t *)c->retry2.p, cnt2, (int32_t *)c->retry_count.p + 12,
+                                              getenv("RMPC_DENSE_CAP") ? atoi(getenv("RMPC_DENSE_CAP")) : 12,
+                                              s, pc));
+            if (prof) {
+                unsigned long long h[64];
+                int32_t cn[16];
+                HIP_TRY(hipMemcpyAsync(h, pc, sizeof(h), hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipMemcpyAsync(cn, c->retry_count.p, sizeof(cn), hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipStreamSynchronize(s));
+                const double r = h[10] ? (double)h[10] : 1.0;
+                fprintf(stderr,
+                        "[dense] in=%d out=%d done=%llu iters(ph1)=%llu ph2=%llu | cycles/robot: stage %.0f "
+                        "gam %.0f h0 %.0f solve %.0f test %.0f ph2 %.0f out %.0f | per ph1 iter: solve %.0f test %.0f"
+                        " | all solves: build %.0f chol %.0f subst %.0f\n",
+                        cn[0], cn[8], h[10], h[8], h[9], h[0] / r, h[1] / r, h[2] / r, h[3] / r, h[4] / r,
+                        h[5] / r, h[6] / r, h[3] / (double)(h[8] ? h[8] : 1), h[4] / (double)(h[8] ? h[8] : 1),
+                        (double)h[11] / r, (double)h[12] / r, (double)h[13] / r);
+            }
+            dbg_sync(s, "dense");
+            left = (const int32_t *)c->retry2.p;
+            left_n = cnt2;
+        }
+        // what remains is rare (cycling beyond both, non-finite data): LDS generic kernel
         HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
                                     step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
-                                    c->ws.p, (const int32_t *)c->retry.p, (const int32_t *)c->retry_count.p,
-                                    s, rmpc_mpc_lds_lanes(L)));
+                                    c->ws.p, left, left_n, s, rmpc_mpc_lds_lanes(L)));
+        dbg_sync(s, "generic");
     }
     return RMPC_OK;
 }

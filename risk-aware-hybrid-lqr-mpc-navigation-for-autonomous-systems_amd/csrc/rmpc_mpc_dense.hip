@@ -1,0 +1,766 @@
+// rmpc_mpc_dense.hip -- wave-per-robot condensed MPC solve (latency-optimised tail solver).
+//
+// The lane-per-robot kernels are throughput machines: one 64-lane wave advances 64 robots
+// at once, but one active-set iteration of ONE robot is ~30 us of dependent fp64 latency.
+// The few robots that need many iterations (those starting inside an obstacle's margin,
+// where the actuator bounds activate in a long cascade; ~1-3% of BASELINE config 3) would
+// hold the whole launch.  This kernel gives each such robot a wave and solves the same QP
+// in condensed form, every iteration a 64-lane parallel computation:
+//
+//   x_k = xf_k + Gam_k z            z = blocked input deviations, n = 2*NB <= 64
+//   F(z) = 1/2 z'H0 z + g0'z + c0 + rho sum_i max(0, c_i - a_i'z)^2,  a_i = Gam_pos,k' n_i
+//   lo <= z <= hi
+//
+// Lane i owns row i of every n x n matrix, in VGPRs: H0 = 2(Gam' diag(Q..Q,P) Gam + E'RE)
+// is built once per robot; each primal-dual active-set iteration adds the active hinge
+// rows (one rank-2 term per step), eliminates the box-fixed components, factors with a
+// right-looking register Cholesky (column j broadcast with v_readlane) and substitutes
+// forward (registers) and backward (L staged once through LDS).  Trajectories come from
+// a redundant uniform forward simulation, gradients from Gam's columns (LDS, lane-
+// contiguous).  The set rules, cycle detection and the projected-Newton/Armijo phase are
+// those of the other kernels, and certification is the same set-reproduction test, so the
+// result is the QP's exact optimum.
+//
+// LTV formulation (mpc_controller.py:345-522) -- the robots handed on by the fast kernel.
+#include "rmpc_device.h"
+#include "rmpc_internal.h"
+#include "rmpc_riccati.h"
+
+#include <cstdlib>
+
+namespace rmpc {
+
+struct DenseArgs {
+    MpcDevParams prm;
+    int no;
+    const double *x0, *x_refs, *u_refs, *obs;
+    int ref_rows, uref_rows;
+    int32_t *step_count;
+    double *u0, *u_seq, *x_pred, *cost;
+    int32_t *status, *iters;
+    uint8_t *slack_used;
+    const int32_t *index, *count;     // robots to solve (device-side length)
+    int32_t *retry, *retry_count;     // not certified / non-finite -> generic kernel
+    unsigned long long *prof;         // optional per-phase cycle counters (diagnostics)
+    int32_t *next;                    // work counter (zeroed before launch)
+    int pdas_cap;                     // phase-1 iterations before projected Newton
+};
+
+// diagnostics: s_memtime deltas per phase, kept in registers, flushed once per robot
+#define DPROF(slot)                                                                   \
+    do {                                                                              \
+        if (prof_on) {                                                                \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();               \
+            pacc[slot] += t_ - tprof;                                                 \
+            tprof = t_;                                                               \
+        }                                                                             \
+    } while (0)
+
+// LDS footprint (doubles) of one robot; n = 2*NB inputs, NT16 = n rounded up to the
+// 16-wide MFMA tile, KS = k-steps (4 rows each) of the hinge product over 2N rows
+__host__ __device__ constexpr int dense_n(int N, int bs) { return 2 * ((N + bs - 1) / bs); }
+__host__ __device__ constexpr int dense_nt16(int N, int bs) { return (dense_n(N, bs) + 15) / 16 * 16; }
+__host__ __device__ constexpr int dense_lds_doubles(int N, int bs, int no) {
+    return (N + 1) * 3 * dense_nt16(N, bs)                     // GAM [(N+1)*3][NT16] (zero pad)
+           + 4 * ((2 * N + 3) / 4) * dense_nt16(N, bs)         // ZM  [4*KS][NT16] hinge-scaled rows
+           + 2 * dense_n(N, bs) * (dense_n(N, bs) + 1)         // H0, MM [n][n+1] (MM doubles as LT)
+           + dense_n(N, bs)                                    // ZB  [n]
+           + 6 * N                                             // STG [6][N]
+           + 3 * (N + 1)                                       // XF  [N+1][3]
+           + 2 * N                                             // FB  [2][N]
+           + 5 * N                                             // WV  [5][N] hinge weights per step
+           + 3 * no * N;                                       // HR  [3][no][N]
+}
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double rdl(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+__device__ __forceinline__ double wmaxr(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+    return v;
+}
+
+template <int N, int BS>
+struct Dense {
+    static constexpr int NB = (N + BS - 1) / BS;
+    static constexpr int n = 2 * NB;
+    static constexpr int NPL = n + 1;
+    static constexpr int NT = (n + 15) / 16, NT16 = NT * 16;
+    static constexpr int KS = (2 * N + 3) / 4;
+
+    const int lane, no, ic;           // ic: this lane's column, clamped below n
+    double *const s0;
+    double *GAM, *ZM, *H0, *MM, *LT, *ZB, *STG, *XF, *FB, *WV, *HR;
+
+    __device__ Dense(double *s, int lane_, int no_)
+        : lane(lane_), no(no_), ic(lane_ < n ? lane_ : n - 1), s0(s) { refresh(); }
+    // Re-derive the LDS views from an opaque offset: the LDS regions are provably disjoint,
+    // so without this the optimiser hoists every loop-invariant LDS load (all of Gam, the
+    // stage data) out of the active-set loop and runs out of VGPRs.
+    __device__ __forceinline__ void refresh() {
+        int o = 0;
+        asm volatile("" : "+v"(o));
+        GAM = s0 + o;
+        ZM = GAM + (N + 1) * 3 * NT16;
+        H0 = ZM + 4 * KS * NT16;
+        MM = H0 + n * NPL;
+        LT = MM;                      // the factor reuses the assembled matrix's space
+        ZB = MM + n * NPL;
+        STG = ZB + n;
+        XF = STG + 6 * N;
+        FB = XF + 3 * (N + 1);
+        WV = FB + 2 * N;
+        HR = WV + 5 * N;
+    }
+    __device__ __forceinline__ double &A0(int k) { return STG[k]; }
+    __device__ __forceinline__ double &A1(int k) { return STG[N + k]; }
+    __device__ __forceinline__ double &B0(int k) { return STG[2 * N + k]; }
+    __device__ __forceinline__ double &B1(int k) { return STG[3 * N + k]; }
+    __device__ __forceinline__ double &US0(int k) { return STG[4 * N + k]; }
+    __device__ __forceinline__ double &US1(int k) { return STG[5 * N + k]; }
+    __device__ __forceinline__ double &HN0(int o, int k) { return HR[o * N + k]; }
+    __device__ __forceinline__ double &HN1(int o, int k) { return HR[(no + o) * N + k]; }
+    __device__ __forceinline__ double &HB(int o, int k) { return HR[(2 * no + o) * N + k]; }
+    __device__ __forceinline__ double &G(int k, int d, int l) { return GAM[(3 * k + d) * NT16 + l]; }
+    // element (i, l) of a symmetric matrix of which only the lower 16x16 tiles are stored
+    static __device__ __forceinline__ double sym(const double *A, int i, int l) {
+        return (l >> 4) <= (i >> 4) ? A[i * NPL + l] : A[l * NPL + i];
+    }
+    // columns of Gam that can be nonzero at step k (inputs of blocks starting before k)
+    static __device__ __forceinline__ int ncols(int k) {
+        return 2 * ((k + BS - 1) / BS) < n ? 2 * ((k + BS - 1) / BS) : n;
+    }
+
+    // x_k of this lane (k = lane <= N) for the inputs in ZB; every lane runs the same
+    // (uniform) forward simulation and keeps its own step
+    __device__ __forceinline__ void traj(double dt, double &y0, double &y1, double &y2) {
+        double x0 = XF[0], x1 = XF[1], x2 = XF[2];
+        y0 = x0; y1 = x1; y2 = x2;
+#pragma unroll 4
+        for (int k = 0; k < N; k++) {
+            const int j = k / BS;
+            const double u0 = ZB[2 * j], u1 = ZB[2 * j + 1];
+            const double n0 = x0 + A0(k) * x2 + B0(k) * u0;
+            const double n1 = x1 + A1(k) * x2 + B1(k) * u0;
+            const double n2 = x2 + dt * u1;
+            x0 = n0; x1 = n1; x2 = n2;
+            if (lane == k + 1) { y0 = x0; y1 = x1; y2 = x2; }
+        }
+    }
+
+    // gradient component (lane i) of the quadratic piece whose per-step hinge forces are in
+    // FB, at the inputs in ZB:  h.z + g0 + Gam_pos,i' f
+    __device__ __forceinline__ double grad(double g0i) {
+        double g = g0i;
+#pragma unroll
+        for (int l = 0; l < n; l++) g += sym(H0, ic, l) * ZB[l];
+#pragma unroll 2
+        for (int k = 1; k < N; k++) g += G(k, 0, ic) * FB[k] + G(k, 1, ic) * FB[N + k];
+        return g;
+    }
+
+    // hinge residual of row (o, k) at position (y0, y1)
+    __device__ __forceinline__ double resid(int o, int k, double y0, double y1) {
+        return HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1;
+    }
+};
+
+template <int N, int BS>
+__device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int64_t b, int lane) {
+    using D = Dense<N, BS>;
+    constexpr int n = D::n, NB = D::NB, NPL = D::NPL;
+    const MpcDevParams &p = a.prm;
+    const int no = a.no;
+    D d(s, lane, no);
+    const double dt = p.dt, rho = p.rho;
+    const double *xr = a.x_refs + (size_t)b * a.ref_rows * 3;
+    const double *ur = a.u_refs + (size_t)b * a.uref_rows * 2;
+    const int ic = d.ic;
+    const bool prof_on = a.prof != nullptr;
+    unsigned long long tprof = prof_on ? __builtin_amdgcn_s_memtime() : 0ull;
+    unsigned long long pacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+
+    // ---- stage data: np.unwrap (numpy order, uniform), linearisation (lane k)
+    double corr = 0.0, prev = xr[2], thk = 0.0, th0 = 0.0;
+    for (int k = 0; k < N; k++) {
+        const double th = xr[3 * k + 2];
+        if (k > 0 && fabs(th - prev) >= RMPC_PI) corr += unwrap_step(prev, th);
+        prev = th;
+        const double thu = th + corr;
+        if (k == 0) th0 = thu;
+        if (k == lane) thk = thu;
+    }
+    int fin = 1;
+    if (lane < N) {
+        const int k = lane;
+        double sn, cs;
+        sincos(thk, &sn, &cs);
+        const double v = ur[2 * k];
+        const double vr = fabs(v) > 0.01 ? v : 0.1;                   // :425
+        d.A0(k) = -vr * sn * dt;
+        d.A1(k) = vr * cs * dt;
+        d.B0(k) = cs * dt;
+        d.B1(k) = sn * dt;
+        d.US0(k) = v;
+        d.US1(k) = ur[2 * k + 1];
+        fin = isfinite(sn + cs + v + ur[2 * k + 1] + xr[3 * k] + xr[3 * k + 1]);
+        for (int o = 0; o < no; o++) {
+            double n0, n1, hb;
+            if (!hinge_row_ltv(xr[3 * k], xr[3 * k + 1], a.obs[3 * o], a.obs[3 * o + 1],
+                               p.d_safe + a.obs[3 * o + 2], n0, n1, hb)) {
+                n0 = 0; n1 = 0; hb = -1e300;                           // row not kept
+            }
+            d.HN0(o, k) = n0;
+            d.HN1(o, k) = n1;
+            d.HB(o, k) = hb;
+        }
+    }
+    double lo = 0, hi = 0;
+    if (lane < n) {                                                   // blocked box (:431-436)
+        const int j = lane >> 1, c = lane & 1;
+        const double lim = c ? p.omega_max : p.v_max;
+        lo = -1e300; hi = 1e300;
+        for (int k = j * BS; k < (j + 1) * BS && k < N; k++) {
+            lo = fmax(lo, -lim - ur[2 * k + c]);
+            hi = fmin(hi, lim - ur[2 * k + c]);
+        }
+    }
+    const double *x0p = a.x0 + 3 * b;
+    const double x0a = th0 + wrap_pi(x0p[2] - th0);                  // :397-401
+    if (lane == 0) fin = fin && isfinite(x0p[0] + x0p[1] + x0a);
+    if (__any(!fin)) {                  // fallback law: the generic kernel owns it
+        if (lane == 0) a.retry[atomicAdd(a.retry_count, 1)] = (int32_t)b;
+        return;
+    }
+    __syncthreads();
+    DPROF(0);
+    // ---- free response (uniform) and the sensitivity column of this lane
+    {
+        double x0 = x0p[0] - xr[0], x1 = x0p[1] - xr[1], x2 = x0a - th0;
+        double g0 = 0, g1 = 0, g2 = 0;
+        const int j = lane < n ? lane >> 1 : -1, c = lane & 1;      // lanes >= n: zero columns
+#pragma unroll 1
+        for (int k = 0; k <= N; k++) {
+            if (lane == k) { d.XF[3 * k] = x0; d.XF[3 * k + 1] = x1; d.XF[3 * k + 2] = x2; }
+            if (lane < D::NT16) { d.G(k, 0, lane) = g0; d.G(k, 1, lane) = g1; d.G(k, 2, lane) = g2; }
+            if (k < N) {
+                const double a0 = d.A0(k), a1 = d.A1(k);
+                const double n0 = x0 + a0 * x2, n1 = x1 + a1 * x2;
+                x0 = n0; x1 = n1;
+                const double e = (k / BS == j) ? 1.0 : 0.0;
+                const double m0 = g0 + a0 * g2 + (c == 0 ? d.B0(k) * e : 0.0);
+                const double m1 = g1 + a1 * g2 + (c == 0 ? d.B1(k) * e : 0.0);
+                const double m2 = g2 + (c == 1 ? dt * e : 0.0);
+                g0 = m0; g1 = m1; g2 = m2;
+            }
+        }
+    }
+    __syncthreads();
+    DPROF(1);
+    // ---- H0 = 2(Gam' W Gam + E'RE) on the matrix cores (lower 16x16 tiles; rows are the
+    // (k, d) state components, K = 3N), and g0 = 2(Gam' W xf + E'R us) per lane
+    {
+        constexpr int NT = D::NT, NT16 = D::NT16, KS0 = (3 * N + 3) / 4;
+        dbl4 acc[NT * (NT + 1) / 2];
+#pragma unroll
+        for (int t = 0; t < NT * (NT + 1) / 2; t++) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+        const int q = lane >> 4, c16 = lane & 15;
+#pragma unroll 1
+        for (int st = 0; st < KS0; st++) {
+            const int kk = 4 * st + q;
+            const bool valid = kk < 3 * N;
+            const int k = 1 + (valid ? kk / 3 : 0), dd = valid ? kk % 3 : 0;
+            const double w = valid ? (k < N ? p.Q[dd] : p.P[dd]) : 0.0;
+            double av[NT], bv[NT];
+#pragma unroll
+            for (int t = 0; t < NT; t++) {
+                bv[t] = d.GAM[(3 * k + dd) * NT16 + 16 * t + c16];
+                av[t] = w * bv[t];
+            }
+            int tt = 0;
+#pragma unroll
+            for (int ti = 0; ti < NT; ti++)
+#pragma unroll
+                for (int tl = 0; tl <= ti; tl++, tt++)
+                    acc[tt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ti], bv[tl], acc[tt], 0, 0, 0);
+        }
+        int tt = 0;
+#pragma unroll
+        for (int ti = 0; ti < NT; ti++)
+#pragma unroll
+            for (int tl = 0; tl <= ti; tl++, tt++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int row = 16 * ti + q + 4 * r, col = 16 * tl + c16;
+                    if (row < n && col < n) {
+                        double v = acc[tt][r];
+                        if (row == col) {
+                            const int jb = row >> 1, cc = row & 1;
+                            int cnt = 0;
+                            for (int k = jb * BS; k < (jb + 1) * BS && k < N; k++) cnt++;
+                            v += p.R[cc] * cnt;
+                        }
+                        d.H0[row * NPL + col] = 2.0 * v;
+                    }
+                }
+    }
+    double g0i = 0.0;
+#pragma unroll 2
+    for (int k = 1; k <= N; k++) {
+        const double *Wd = k < N ? p.Q : p.P;
+        g0i += Wd[0] * d.G(k, 0, ic) * d.XF[3 * k] + Wd[1] * d.G(k, 1, ic) * d.XF[3 * k + 1] +
+               Wd[2] * d.G(k, 2, ic) * d.XF[3 * k + 2];
+    }
+    {
+        const int j = ic >> 1, c = ic & 1;
+        double us = 0;
+        for (int k = j * BS; k < (j + 1) * BS && k < N; k++) us += ur[2 * k + c];
+        g0i = 2.0 * (g0i + p.R[c] * us);
+    }
+    // the padded rows of the hinge product stay zero
+    for (int e = lane; e < (4 * D::KS - 2 * N) * D::NT16; e += 64) d.ZM[2 * N * D::NT16 + e] = 0.0;
+    __syncthreads();
+
+    // ---- PDAS state: hinge flags of step k on lane k, box state of component i on lane i
+    uint32_t hf = 0;
+    int bf = 0;
+    double zc = 0.0;              // candidate of the last solve (lane i)
+    const double eps_h = 1e-14, eps_b = 1e-13;
+
+    // zc <- minimiser of the quadratic piece (hf, bf) with fixed components at their bounds
+    auto solve = [&]() __attribute__((always_inline)) {
+        d.refresh();
+        constexpr int NT = D::NT, NT16 = D::NT16, KS = D::KS;
+        // per-step hinge weights W_k = 2 rho sum n n', v_k = -2 rho sum c n (lane k)
+        if (lane < N) {
+            double w00 = 0, w01 = 0, w11 = 0, v0 = 0, v1 = 0;
+            if (lane > 0 && hf) {
+                for (int o = 0; o < no; o++) {
+                    if (!((hf >> o) & 1u)) continue;
+                    const double n0 = d.HN0(o, lane), n1 = d.HN1(o, lane);
+                    const double ci = d.HB(o, lane) - n0 * d.XF[3 * lane] - n1 * d.XF[3 * lane + 1];
+                    w00 += 2 * rho * n0 * n0;
+                    w01 += 2 * rho * n0 * n1;
+                    w11 += 2 * rho * n1 * n1;
+                    v0 -= 2 * rho * ci * n0;
+                    v1 -= 2 * rho * ci * n1;
+                }
+            }
+            d.WV[lane] = w00; d.WV[N + lane] = w01; d.WV[2 * N + lane] = w11;
+            d.WV[3 * N + lane] = v0; d.WV[4 * N + lane] = v1;
+        }
+        __syncthreads();
+        // Z = blockdiag(W_k) Gam_pos (lane = column)
+        if (lane < NT16) {
+#pragma unroll 4
+            for (int k = 0; k < N; k++) {
+                const double gx = d.G(k, 0, lane), gy = d.G(k, 1, lane);
+                const double w00 = d.WV[k], w01 = d.WV[N + k], w11 = d.WV[2 * N + k];
+                d.ZM[(2 * k) * NT16 + lane] = w00 * gx + w01 * gy;
+                d.ZM[(2 * k + 1) * NT16 + lane] = w01 * gx + w11 * gy;
+            }
+        }
+        __syncthreads();
+        // M = H0 + Gam_pos' Z on the matrix cores (lower tiles), rows to MM
+        {
+            const int q = lane >> 4, c16 = lane & 15;
+            dbl4 acc[NT * (NT + 1) / 2];
+            int tt = 0;
+#pragma unroll
+            for (int ti = 0; ti < NT; ti++)
+#pragma unroll
+                for (int tl = 0; tl <= ti; tl++, tt++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int row = 16 * ti + q + 4 * r, col = 16 * tl + c16;
+                        acc[tt][r] = (row < n && col < n) ? d.H0[row * NPL + col] : 0.0;
+                    }
+#pragma unroll 2
+            for (int st = 0; st < KS; st++) {
+                const int kk = 4 * st + q;                 // row (k, comp) = (kk >> 1, kk & 1)
+                const int grow = 3 * (kk >> 1) + (kk & 1);
+                double av[NT], bv[NT];
+#pragma unroll
+                for (int t = 0; t < NT; t++) {
+                    av[t] = d.GAM[grow * NT16 + 16 * t + c16];
+                    bv[t] = d.ZM[kk * NT16 + 16 * t + c16];
+                }
+                tt = 0;
+#pragma unroll
+                for (int ti = 0; ti < NT; ti++)
+#pragma unroll
+                    for (int tl = 0; tl <= ti; tl++, tt++)
+                        acc[tt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ti], bv[tl], acc[tt], 0, 0, 0);
+            }
+            tt = 0;
+#pragma unroll
+            for (int ti = 0; ti < NT; ti++)
+#pragma unroll
+                for (int tl = 0; tl <= ti; tl++, tt++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int row = 16 * ti + q + 4 * r, col = 16 * tl + c16;
+                        if (row < n && col < n) d.MM[row * NPL + col] = acc[tt][r];
+                    }
+        }
+        __syncthreads();
+        double m[n];
+#pragma unroll
+        for (int l = 0; l < n; l++) m[l] = D::sym(d.MM, ic, l);
+        double gi = g0i;
+#pragma unroll 2
+        for (int k = 1; k < N; k++) gi += d.G(k, 0, ic) * d.WV[3 * N + k] + d.G(k, 1, ic) * d.WV[4 * N + k];
+        __syncthreads();              // MM is rewritten as LT below
+        DPROF(7);
+        // box-fixed components: value to the right-hand side, identity rows/columns
+        const double fv = bf == 1 ? lo : (bf == 2 ? hi : 0.0);
+        const uint64_t fixm = __ballot(lane < n && bf != 0);
+        double r = -gi;
+#pragma unroll
+        for (int l = 0; l < n; l++)
+            if ((fixm >> l) & 1ull) r -= m[l] * rdl(fv, l);
+#pragma unroll
+        for (int l = 0; l < n; l++)
+            if (((fixm >> l) & 1ull) || bf != 0) m[l] = (l == lane) ? 1.0 : 0.0;
+        if (bf != 0) r = fv;
+        // right-looking Cholesky: lane i keeps L[i][0..i] in m (upper part: don't care)
+        // (a fixed component's column is e_j: nothing to eliminate, pivot 1)
+        double invd = 1.0;
+#pragma unroll
+        for (int j = 0; j < n; j++) {
+            if ((fixm >> j) & 1ull) continue;
+            const double dj = rdl(m[j], j);
+            const double piv = sqrt(dj), ip = 1.0 / piv;
+            if (lane == j) { m[j] = piv; invd = ip; }
+            else m[j] *= ip;
+#pragma unroll
+            for (int k = j + 1; k < n; k++)
+                if (!((fixm >> k) & 1ull)) m[k] -= m[j] * rdl(m[j], k);
+        }
+        DPROF(8);
+        // forward: L y = r
+#pragma unroll
+        for (int j = 0; j < n; j++) {
+            const double yj = rdl(r * invd, j);
+            if (lane == j) r = yj;
+            else if (lane > j) r -= m[j] * yj;
+        }
+        // backward: L' z = y (rows of L through LDS, read column-wise)
+        if (lane < n) {
+#pragma unroll
+            for (int l = 0; l < n; l++)
+                if (l <= lane) d.LT[lane * NPL + l] = m[l];
+        }
+        __syncthreads();
+        double zz = 0.0;
+#pragma unroll
+        for (int j = n - 1; j >= 0; j--) {
+            const double zj = rdl(r * invd, j);
+            if (lane == j) zz = zj;
+            else if (lane < j) r -= d.LT[j * NPL + lane] * zj;
+        }
+        zc = zz;
+        __syncthreads();
+        DPROF(9);
+    };
+
+    // PDAS test of the candidate zc under (hf, bf); mode 0 also updates the sets.
+    // Returns 1 if any set changes.
+    auto pdas_test = [&](int mode) __attribute__((always_inline)) -> int {
+        d.refresh();
+        if (lane < n) d.ZB[lane] = zc;
+        __syncthreads();
+        double y0, y1, y2;
+        d.traj(dt, y0, y1, y2);
+        double f0 = 0, f1 = 0;
+        uint32_t nh = hf;
+        if (lane >= 1 && lane < N) {
+            for (int o = 0; o < no; o++) {
+                const double r = d.resid(o, lane, y0, y1);
+                const uint32_t act = (hf >> o) & 1u;
+                if (act) {
+                    f0 -= 2 * rho * r * d.HN0(o, lane);
+                    f1 -= 2 * rho * r * d.HN1(o, lane);
+                }
+                const uint32_t na = act ? (r > -eps_h) : (r > eps_h);
+                if (na != act) nh ^= (1u << o);
+            }
+        }
+        if (lane < N) { d.FB[lane] = f0; d.FB[N + lane] = f1; }
+        __syncthreads();
+        const double lam = d.grad(g0i);     // box multipliers of the fixed components
+        int nb = bf;
+        if (lane < n) nb = box_rule(bf, bf ? lam : zc, lo, hi, eps_b);
+        const int any = __any((nh != hf) || (nb != bf));
+        if (mode == 0) { hf = nh; bf = nb; }
+        __syncthreads();
+        return any;
+    };
+
+    // objective (full cost, constants included) at the inputs in ZB
+    auto objective = [&]() __attribute__((always_inline)) -> double {
+        d.refresh();
+        double y0, y1, y2;
+        d.traj(dt, y0, y1, y2);
+        double jl = 0.0;
+        if (lane <= N) {
+            const double *Wd = lane < N ? p.Q : p.P;
+            jl = Wd[0] * y0 * y0 + Wd[1] * y1 * y1 + Wd[2] * y2 * y2;
+            if (lane < N) {
+                const int j = lane / BS;
+                const double uu0 = d.ZB[2 * j] + d.US0(lane), uu1 = d.ZB[2 * j + 1] + d.US1(lane);
+                jl += p.R[0] * uu0 * uu0 + p.R[1] * uu1 * uu1;
+                for (int o = 0; o < no; o++) {
+                    const double r = d.resid(o, lane, y0, y1);
+                    if (r > 0) jl += rho * r * r;
+                }
+            }
+        }
+        return wsum(jl);
+    };
+
+    // true gradient (rows with r > 0) at the inputs in ZB
+    auto true_grad = [&]() __attribute__((always_inline)) -> double {
+        d.refresh();
+        double y0, y1, y2;
+        d.traj(dt, y0, y1, y2);
+        double f0 = 0, f1 = 0;
+        if (lane >= 1 && lane < N) {
+            for (int o = 0; o < no; o++) {
+                const double r = d.resid(o, lane, y0, y1);
+                if (r > 0) {
+                    f0 -= 2 * rho * r * d.HN0(o, lane);
+                    f1 -= 2 * rho * r * d.HN1(o, lane);
+                }
+            }
+        }
+        __syncthreads();
+        if (lane < N) { d.FB[lane] = f0; d.FB[N + lane] = f1; }
+        __syncthreads();
+        const double g = d.grad(g0i);
+        __syncthreads();
+        return g;
+    };
+
+    // ---- phase 1: PDAS (cap + cycle detection)
+    int it = 0, cert = 0;
+    const int max_iter = p.max_iter;
+    uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    while (it < max_iter && it < a.pdas_cap) {
+        it++;
+        solve();
+        DPROF(3);
+        const int chg = pdas_test(0);
+        DPROF(4);
+        if (!chg) { cert = 1; break; }
+        // signature of (hinge flags, box states): the FNV walk of the other kernels
+        uint64_t sig = 1469598103934665603ull;
+        for (int k = 0; k < N; k++)
+            sig = (sig ^ (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hf, k)) * 1099511628211ull;
+        for (int j = 0; j < NB; j++) {
+            const int w = __builtin_amdgcn_readlane(bf, 2 * j) | (__builtin_amdgcn_readlane(bf, 2 * j + 1) << 2);
+            sig = (sig ^ (uint64_t)w) * 1099511628211ull;
+        }
+        if (sig == s0 || sig == s1 || sig == s2 || sig == s3) break;
+        s3 = s2; s2 = s1; s1 = s0; s0 = sig;
+    }
+    const int it1 = it;
+    // ---- phase 2: projected Newton + Armijo from the projected last iterate
+    if (!cert && it < max_iter) {
+        double z = lane < n ? clampv(zc, lo, hi) : 0.0;
+        if (lane < n) d.ZB[lane] = z;
+        __syncthreads();
+        double F = objective();
+        while (it < max_iter) {
+            const double g = true_grad();                 // ZB holds z
+            const double wl = lane < n ? fabs(z - clampv(z - g, lo, hi)) : 0.0;
+            const double eps = fmin(1e-6, wmaxr(wl));
+            {   // sets from the current point
+                d.refresh();
+                double y0, y1, y2;
+                d.traj(dt, y0, y1, y2);
+                uint32_t nh = 0;
+                if (lane >= 1 && lane < N)
+                    for (int o = 0; o < no; o++)
+                        if (d.resid(o, lane, y0, y1) > 0) nh |= 1u << o;
+                hf = nh;
+                bf = lane < n ? ((z <= lo + eps && g > 0) ? 1 : ((z >= hi - eps && g < 0) ? 2 : 0)) : 0;
+            }
+            it++;
+            solve();
+            if (!pdas_test(1)) { cert = 1; break; }
+            // Armijo along the projection arc
+            if (lane < n) d.ZB[lane] = z;
+            __syncthreads();
+            const double gz = true_grad();
+            double Ft = F, zt = z, alpha = 1.0;
+            int acc = 0;
+            for (int ls = 0; ls < 40; ls++) {
+                zt = lane < n ? clampv(z + alpha * (zc - z), lo, hi) : 0.0;
+                const double gd = wsum(lane < n ? gz * (zt - z) : 0.0);
+                if (lane < n) d.ZB[lane] = zt;
+                __syncthreads();
+                Ft = objective();
+                __syncthreads();
+                if (Ft <= F + 1e-4 * gd) { acc = 1; break; }
+                alpha *= 0.5;
+            }
+            if (!acc) break;
+            z = zt;                                       // ZB holds zt == z
+            F = Ft;
+        }
+    }
+    DPROF(5);
+    if (!cert) {
+        if (lane == 0) a.retry[atomicAdd(a.retry_count, 1)] = (int32_t)b;
+        return;
+    }
+    // ---- outputs from the certified candidate (mpc_controller.py:484-520)
+    d.refresh();
+    if (lane < n) d.ZB[lane] = zc;
+    __syncthreads();
+    double y0, y1, y2;
+    d.traj(dt, y0, y1, y2);
+    double jl = 0.0;
+    int used = 0;
+    if (lane <= N) {
+        const double *Wd = lane < N ? p.Q : p.P;
+        jl = Wd[0] * y0 * y0 + Wd[1] * y1 * y1 + Wd[2] * y2 * y2;
+        if (lane < N) {
+            const int j = lane / BS;
+            const double uu0 = d.ZB[2 * j] + d.US0(lane), uu1 = d.ZB[2 * j + 1] + d.US1(lane);
+            jl += p.R[0] * uu0 * uu0 + p.R[1] * uu1 * uu1;
+            for (int o = 0; o < no; o++) {
+                const double r = d.resid(o, lane, y0, y1);
+                if (r > 0) {
+                    jl += rho * r * r;
+                    if (r > 1e-6) used = 1;                            // :485
+                }
+            }
+        }
+    }
+    const double J = wsum(jl);
+    if (!isfinite(J)) {
+        if (lane == 0) a.retry[atomicAdd(a.retry_count, 1)] = (int32_t)b;
+        return;
+    }
+    if (a.x_pred && lane <= N) {        // x_refs + dx, not unwrapped (:497)
+        double *xp = a.x_pred + ((size_t)b * (N + 1) + lane) * 3;
+        xp[0] = y0 + xr[3 * lane];
+        xp[1] = y1 + xr[3 * lane + 1];
+        xp[2] = y2 + xr[3 * lane + 2];
+    }
+    const int any_used = __any(used);
+    const int sc = a.step_count ? a.step_count[b] : 0;
+    if (lane < N) {
+        const int j = lane / BS;
+        const double v0 = d.ZB[2 * j] + d.US0(lane);
+        double v1 = d.ZB[2 * j + 1] + d.US1(lane);
+        if (lane == 0 && sc < p.ramp_up_steps) {                      // :502-505
+            const double lim = p.omega_max * ((double)(sc + 1) / (double)p.ramp_up_steps);
+            v1 = clampv(v1, -lim, lim);
+        }
+        if (a.u_seq) {
+            a.u_seq[((size_t)b * N + lane) * 2] = v0;
+            a.u_seq[((size_t)b * N + lane) * 2 + 1] = v1;
+        }
+        if (lane == 0) {
+            a.u0[2 * b] = v0;
+            a.u0[2 * b + 1] = v1;
+        }
+    }
+    if (lane == 0) {
+        if (a.step_count) a.step_count[b] = sc + 1;                   // :507
+        if (a.cost) a.cost[b] = J;
+        if (a.slack_used) a.slack_used[b] = (uint8_t)any_used;
+        a.status[b] = RMPC_OPTIMAL;
+        if (a.iters) a.iters[b] = it;
+    }
+    DPROF(6);
+    if (prof_on && lane == 0) {
+        for (int q = 0; q < 7; q++) atomicAdd(a.prof + q, pacc[q]);
+        for (int q = 7; q < 10; q++) atomicAdd(a.prof + 4 + q, pacc[q]);
+        atomicAdd(a.prof + 8, (unsigned long long)it1);
+        atomicAdd(a.prof + 9, (unsigned long long)(it > it1));
+        atomicAdd(a.prof + 10, 1ull);
+    }
+}
+
+// Persistent: each workgroup takes the next list entry from a device counter until the
+// list (length written by the fast kernel earlier on the same stream) is exhausted --
+// dynamic, because per-robot cost varies by 10x and more.
+template <int N, int BS>
+__global__ __launch_bounds__(64, 1) void mpc_dense_kernel(DenseArgs a) {
+    extern __shared__ double s[];
+    const int lane = threadIdx.x;
+    const int cnt = *a.count;
+    for (int t = blockIdx.x; t < cnt; t += gridDim.x) {
+        __syncthreads();                // LDS of the previous robot is dead
+        dense_solve<N, BS>(a, s, a.index[t], lane);
+    }
+}
+
+}  // namespace rmpc
+
+using namespace rmpc;
+
+bool rmpc_mpc_dense_supported(int N, int bs, int no) {
+    const bool inst = (bs == 1 && (N == 6 || N == 10 || N == 20)) || (bs == 2 && N == 6);
+    return inst && no <= 16 && (size_t)dense_lds_doubles(N, bs, no) * sizeof(double) <= 160 * 1024;
+}
+
+hipError_t rmpc_launch_mpc_dense_f64(const MpcDevParams &prm, int N, int bs, int no, int64_t capacity,
+                                     const double *x0, const double *x_refs, int ref_rows,
+                                     const double *u_refs, int uref_rows, const double *obstacles,
+                                     int32_t *step_count, double *u0, double *u_seq, double *x_pred,
+                                     double *cost, int32_t *status, uint8_t *slack_used, int32_t *iters,
+                                     const int32_t *index, const int32_t *count, int32_t *retry,
+                                     int32_t *retry_count, int32_t *next, int pdas_cap, hipStream_t stream,
+                                     unsigned long long *prof) {
+    if (capacity <= 0) return hipSuccess;
+    if (!rmpc_mpc_dense_supported(N, bs, no)) return hipErrorInvalidValue;
+    DenseArgs a;
+    a.prm = prm;
+    a.no = no;
+    a.x0 = x0; a.x_refs = x_refs; a.u_refs = u_refs; a.obs = obstacles;
+    a.ref_rows = ref_rows; a.uref_rows = uref_rows;
+    a.step_count = step_count;
+    a.u0 = u0; a.u_seq = u_seq; a.x_pred = x_pred; a.cost = cost;
+    a.status = status; a.iters = iters; a.slack_used = slack_used;
+    a.index = index; a.count = count; a.retry = retry; a.retry_count = retry_count;
+    a.prof = prof;
+    a.next = next;
+    a.pdas_cap = pdas_cap < RMPC_PDAS_ITERS ? pdas_cap : RMPC_PDAS_ITERS;
+    const size_t lds = (size_t)dense_lds_doubles(N, bs, no) * sizeof(double);
+    // one wave per SIMD (VGPR-bound): 4 per CU fill the chip, more only queue
+    const int per_cu = getenv("RMPC_DENSE_WPC") ? atoi(getenv("RMPC_DENSE_WPC")) : 4;
+    const int64_t gmax = (int64_t)256 * (per_cu > 0 ? per_cu : 4);
+    const int64_t grid = capacity < gmax ? capacity : gmax;
+    const dim3 g((unsigned)grid), blk(64);
+    const void *fn = (bs == 1 && N == 20)   ? (const void *)mpc_dense_kernel<20, 1>
+                     : (bs == 1 && N == 10) ? (const void *)mpc_dense_kernel<10, 1>
+                     : (bs == 1 && N == 6)  ? (const void *)mpc_dense_kernel<6, 1>
+                                            : (const void *)mpc_dense_kernel<6, 2>;
+    if (lds > 64 * 1024) {
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_dense_kernel<20, 1>), g, blk, lds, stream, a);
+    else if (bs == 1 && N == 10) hipLaunchKernelGGL((mpc_dense_kernel<10, 1>), g, blk, lds, stream, a);
+    else if (bs == 1 && N == 6) hipLaunchKernelGGL((mpc_dense_kernel<6, 1>), g, blk, lds, stream, a);
+    else hipLaunchKernelGGL((mpc_dense_kernel<6, 2>), g, blk, lds, stream, a);
+    return hipGetLastError();
+}

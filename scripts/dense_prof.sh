@@ -1,0 +1,10 @@
+#!/bin/bash
+# per-phase cycle counters of the dense tail kernel (RMPC_DENSE_PROF) for a few bench steps
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+tag=${1:-dp}; shift
+for v in "$@"; do
+  [ "$v" = "-" ] && v=""
+  echo "== [$v]"
+  env RMPC_DENSE_PROF=1 $v timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/${tag}.json 2>gpurun_out/${tag}.err || exit $?
+  grep "\[dense\]" gpurun_out/${tag}.err | tail -2
+done

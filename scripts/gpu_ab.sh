@@ -1,0 +1,21 @@
+#!/bin/bash
+# GPU parity tests under alternative routing env settings, then a bench A/B.
+# Usage: gpu_ab.sh TAG "ENV1" "ENV2" ...   (each ENV: space-separated VAR=val, or "-")
+# pytest exit 1 (test failures) continues; anything else (fault, abort, timeout) stops.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+tag=${1:-ab}; shift
+i=0
+for v in "$@"; do
+  i=$((i+1)); [ "$v" = "-" ] && v=""
+  echo "== tests [$v]"
+  env $v timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider -x ${PYTEST_ARGS} > gpurun_out/${tag}_t$i.log 2>&1
+  rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/${tag}_t$i.log
+  [ $rc -le 1 ] || exit $rc
+done
+i=0
+for v in "$@"; do
+  i=$((i+1)); [ "$v" = "-" ] && v=""
+  echo "== bench [$v]"
+  env $v timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/${tag}_b$i.json 2>gpurun_out/${tag}_b$i.err || exit $?
+  python -c "import json;d=json.load(open('gpurun_out/${tag}_b$i.json'));print('value %.3e ms/step %.3f'%(d['value'],d['ms_per_step']), d.get('solver'))"
+done
