@@ -125,6 +125,12 @@ int rmpc_ctx_create(int device_id, RmpcCtx **out);
 int rmpc_ctx_destroy(RmpcCtx *ctx);
 int rmpc_ctx_synchronize(RmpcCtx *ctx);
 int rmpc_device_count(int *count);
+/* diagnostics: with timing on, each MPC launch on the lane-per-robot path records events
+ * around its three stages; rmpc_mpc_stage_times waits for the last launch's events and
+ * returns their device times in ms: out3[0] lane-per-robot kernel, out3[1] wave-per-robot
+ * tail kernel, out3[2] generic kernel on what is left. */
+int rmpc_ctx_set_timing(RmpcCtx *ctx, int32_t on);
+int rmpc_mpc_stage_times(RmpcCtx *ctx, double *out3);
 
 /* ---- MPC --------------------------------------------------------------------------------
  * x0        [B][3]

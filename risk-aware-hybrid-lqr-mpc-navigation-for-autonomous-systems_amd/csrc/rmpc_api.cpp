@@ -76,6 +76,11 @@ struct RmpcCtx {
     DevBuf stage[SB_COUNT];    // staging buffers for host-pointer entry points
     DevBuf idx_lqr, idx_mpc, counts, hyb_status;
     DevBuf fast_gains, fast_usol, retry, retry2, retry_count, prof;
+    // stage timing of the last MPC launch (rmpc_ctx_set_timing): events before/after
+    // the lane-per-robot, wave-per-robot and generic stages
+    bool timing = false;
+    bool timed = false;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     std::mutex mu;
 };
 
@@ -123,6 +128,8 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     c->fast_gains.release();
     c->fast_usol.release();
     c->retry.release();
+    for (auto &e : c->ev)
+        if (e) (void)hipEventDestroy(e);
     c->retry2.release();
     c->prof.release();
     c->retry_count.release();
@@ -134,6 +141,30 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
 int rmpc_ctx_synchronize(RmpcCtx *c) {
     if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return RMPC_OK;
+}
+
+int rmpc_ctx_set_timing(RmpcCtx *c, int32_t on) {
+    if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
+    HIP_TRY(hipSetDevice(c->device));
+    if (on)
+        for (auto &e : c->ev)
+            if (!e) HIP_TRY(hipEventCreate(&e));
+    c->timing = on != 0;
+    c->timed = false;
+    return RMPC_OK;
+}
+
+int rmpc_mpc_stage_times(RmpcCtx *c, double *out3) {
+    if (!c || !out3) return fail(RMPC_EINVAL, "ctx or out is NULL");
+    if (!c->timed) return fail(RMPC_EINVAL, "no timed MPC launch on this context (rmpc_ctx_set_timing)");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipEventSynchronize(c->ev[3]));
+    for (int i = 0; i < 3; i++) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]));
+        out3[i] = ms;
+    }
     return RMPC_OK;
 }
 
@@ -265,7 +296,9 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         a.retry = (int32_t *)c->retry.p;
         a.retry_count = (int32_t *)c->retry_count.p;
         a.pdas_cap = getenv("RMPC_FAST_CAP") ? atoi(getenv("RMPC_FAST_CAP")) : 10;
+        if (c->timing) HIP_TRY(hipEventRecord(c->ev[0], s));
         HIP_TRY(rmpc_launch_mpc_fast_f64(a, p->horizon, bs, s));
+        if (c->timing) HIP_TRY(hipEventRecord(c->ev[1], s));
         dbg_sync(s, "fast");
         const int32_t *left = (const int32_t *)c->retry.p;
         const int32_t *left_n = (const int32_t *)c->retry_count.p;
@@ -306,10 +339,15 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             left = (const int32_t *)c->retry2.p;
             left_n = cnt2;
         }
+        if (c->timing) HIP_TRY(hipEventRecord(c->ev[2], s));
         // what remains is rare (cycling beyond both, non-finite data): LDS generic kernel
         HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
                                     step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
                                     c->ws.p, left, left_n, s, rmpc_mpc_lds_lanes(L)));
+        if (c->timing) {
+            HIP_TRY(hipEventRecord(c->ev[3], s));
+            c->timed = true;
+        }
         dbg_sync(s, "generic");
     }
     return RMPC_OK;

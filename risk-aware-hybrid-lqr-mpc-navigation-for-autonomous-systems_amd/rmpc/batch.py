@@ -196,3 +196,17 @@ def figure8_batch(t0, rows, A=2.0, a=0.5, dt=0.02, device=0):
     check(lib.rmpc_figure8_batch(nat.context(device), B, ptr(t0), int(rows), A, a, dt, ptr(xr),
                                  ptr(ur)), "rmpc_figure8_batch")
     return xr, ur
+
+
+def set_stage_timing(on=True, device=0):
+    """Diagnostics: record per-stage device time of each MPC launch on `device`."""
+    lib = nat.load()
+    check(lib.rmpc_ctx_set_timing(nat.context(device), int(bool(on))), "rmpc_ctx_set_timing")
+
+
+def mpc_stage_times(device=0):
+    """Device ms of the last MPC launch: (lane-per-robot, wave-per-robot tail, generic)."""
+    lib = nat.load()
+    out = (C.c_double * 3)()
+    check(lib.rmpc_mpc_stage_times(nat.context(device), out), "rmpc_mpc_stage_times")
+    return tuple(out)

@@ -50,3 +50,18 @@ def noise_for(lo, hi, seed, sigma=(0.05, 0.05, 0.1)):
     b0 = (lo // 65536) * 65536
     full = _noise_aligned(b0, hi, seed, sigma)
     return full[lo - b0:]
+
+
+def aggregate(dist, elapsed, counts, device="cpu"):
+    """Cross-rank reduction of one bench run (the only collectives of the multi-GPU bench):
+    the slowest rank's elapsed time (MAX) and the per-status robot counts (SUM).
+    `dist` is torch.distributed (or None for a single process); tensors live on `device`
+    (cuda for the RCCL backend, cpu for gloo)."""
+    if dist is None:
+        return float(elapsed), [int(c) for c in counts]
+    import torch
+    tt = torch.tensor([float(elapsed)], dtype=torch.float64, device=device)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    cc = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=device)
+    dist.all_reduce(cc)
+    return float(tt.item()), [int(v) for v in cc.tolist()]
