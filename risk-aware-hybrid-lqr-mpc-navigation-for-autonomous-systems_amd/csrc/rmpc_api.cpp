@@ -75,7 +75,7 @@ struct RmpcCtx {
     DevBuf ws;                 // solver workspace
     DevBuf stage[SB_COUNT];    // staging buffers for host-pointer entry points
     DevBuf idx_lqr, idx_mpc, counts, hyb_status;
-    DevBuf fast_gains, fast_usol, retry, retry2, retry_count, prof;
+    DevBuf fast_gains, fast_usol, retry, retry2, retry_count, prof, retry_sets;
     // stage timing of the last MPC launch (rmpc_ctx_set_timing): events before/after
     // the lane-per-robot, wave-per-robot and generic stages
     bool timing = false;
@@ -131,6 +131,7 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
     c->retry2.release();
+    c->retry_sets.release();
     c->prof.release();
     c->retry_count.release();
     (void)hipStreamDestroy(c->stream);
@@ -296,6 +297,11 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         a.retry = (int32_t *)c->retry.p;
         a.retry_count = (int32_t *)c->retry_count.p;
         a.pdas_cap = getenv("RMPC_FAST_CAP") ? atoi(getenv("RMPC_FAST_CAP")) : 10;
+        const bool warm = !getenv("RMPC_COLD_TAIL");
+        if (warm) {
+            HIP_TRY(c->retry_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
+            a.retry_sets = (uint32_t *)c->retry_sets.p;
+        }
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[0], s));
         HIP_TRY(rmpc_launch_mpc_fast_f64(a, p->horizon, bs, s));
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[1], s));
@@ -319,7 +325,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                                               status, slack_used, iters, left, left_n,
                                               (int32_t *)c->retry2.p, cnt2, (int32_t *)c->retry_count.p + 12,
                                               getenv("RMPC_DENSE_CAP") ? atoi(getenv("RMPC_DENSE_CAP")) : 12,
-                                              s, pc));
+                                              a.retry_sets, s, pc));
             if (prof) {
                 unsigned long long h[64];
                 int32_t cn[16];

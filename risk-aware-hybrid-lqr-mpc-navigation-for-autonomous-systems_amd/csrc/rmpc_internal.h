@@ -41,8 +41,10 @@ struct MpcFastArgs {
     uint8_t *slack_used;
     double2 *gains, *usol;           // per-wave tiles
     const int32_t *index, *count;    // optional robot index list (device-side length)
-    int32_t *retry, *retry_count;    // robots handed to the generic kernel
+    int32_t *retry, *retry_count;    // robots handed to the next stage
     int pdas_cap;                    // PDAS solves before a robot is handed on
+    uint32_t *retry_sets;            // per retry slot: hinge flags [N], box states [NB], iters
+                                     // (warm start of the next stage; may be null)
 };
 
 bool rmpc_mpc_fast_supported(int N, int bs);
@@ -53,7 +55,8 @@ hipError_t rmpc_launch_mpc_dense_f64(const MpcDevParams &prm, int N, int bs, int
                                      int32_t *step_count, double *u0, double *u_seq, double *x_pred,
                                      double *cost, int32_t *status, uint8_t *slack_used, int32_t *iters,
                                      const int32_t *index, const int32_t *count, int32_t *retry,
-                                     int32_t *retry_count, int32_t *next, int pdas_cap, hipStream_t stream,
+                                     int32_t *retry_count, int32_t *next, int pdas_cap,
+                                     const uint32_t *warm, hipStream_t stream,
                                      unsigned long long *prof = nullptr);
 hipError_t rmpc_launch_mpc_fast_f64(const MpcFastArgs &a, int N, int bs, hipStream_t stream);
 

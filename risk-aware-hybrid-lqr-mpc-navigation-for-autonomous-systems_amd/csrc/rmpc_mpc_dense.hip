@@ -43,6 +43,8 @@ struct DenseArgs {
     int32_t *retry, *retry_count;     // not certified / non-finite -> generic kernel
     unsigned long long *prof;         // optional per-phase cycle counters (diagnostics)
     int32_t *next;                    // work counter (zeroed before launch)
+    const uint32_t *warm;             // per list entry: hinge flags [N], box states [NB], iters
+                                      // of the previous stage (null: cold start)
     int pdas_cap;                     // phase-1 iterations before projected Newton
 };
 
@@ -179,7 +181,8 @@ struct Dense {
 };
 
 template <int N, int BS>
-__device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int64_t b, int lane) {
+__device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t, int lane) {
+    const int64_t b = a.index[t];
     using D = Dense<N, BS>;
     constexpr int n = D::n, NB = D::NB, NPL = D::NPL;
     const MpcDevParams &p = a.prm;
@@ -337,6 +340,13 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int64
     // ---- PDAS state: hinge flags of step k on lane k, box state of component i on lane i
     uint32_t hf = 0;
     int bf = 0;
+    int it0 = 0;                  // iterations of the previous stage (reported in iters)
+    if (a.warm) {                 // continue from the previous stage's active set
+        const uint32_t *ws = a.warm + (size_t)t * (N + NB + 1);
+        if (lane > 0 && lane < N) hf = ws[lane];
+        if (lane < n) bf = (int)((ws[N + (lane >> 1)] >> (2 * (lane & 1))) & 3u);
+        it0 = (int)ws[N + NB];
+    }
     double zc = 0.0;              // candidate of the last solve (lane i)
     const double eps_h = 1e-14, eps_b = 1e-13;
 
@@ -687,7 +697,7 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int64
         if (a.cost) a.cost[b] = J;
         if (a.slack_used) a.slack_used[b] = (uint8_t)any_used;
         a.status[b] = RMPC_OPTIMAL;
-        if (a.iters) a.iters[b] = it;
+        if (a.iters) a.iters[b] = it0 + it;
     }
     DPROF(6);
     if (prof_on && lane == 0) {
@@ -709,7 +719,7 @@ __global__ __launch_bounds__(64, 1) void mpc_dense_kernel(DenseArgs a) {
     const int cnt = *a.count;
     for (int t = blockIdx.x; t < cnt; t += gridDim.x) {
         __syncthreads();                // LDS of the previous robot is dead
-        dense_solve<N, BS>(a, s, a.index[t], lane);
+        dense_solve<N, BS>(a, s, t, lane);
     }
 }
 
@@ -728,8 +738,8 @@ hipError_t rmpc_launch_mpc_dense_f64(const MpcDevParams &prm, int N, int bs, int
                                      int32_t *step_count, double *u0, double *u_seq, double *x_pred,
                                      double *cost, int32_t *status, uint8_t *slack_used, int32_t *iters,
                                      const int32_t *index, const int32_t *count, int32_t *retry,
-                                     int32_t *retry_count, int32_t *next, int pdas_cap, hipStream_t stream,
-                                     unsigned long long *prof) {
+                                     int32_t *retry_count, int32_t *next, int pdas_cap,
+                                     const uint32_t *warm, hipStream_t stream, unsigned long long *prof) {
     if (capacity <= 0) return hipSuccess;
     if (!rmpc_mpc_dense_supported(N, bs, no)) return hipErrorInvalidValue;
     DenseArgs a;
@@ -743,6 +753,7 @@ hipError_t rmpc_launch_mpc_dense_f64(const MpcDevParams &prm, int N, int bs, int
     a.index = index; a.count = count; a.retry = retry; a.retry_count = retry_count;
     a.prof = prof;
     a.next = next;
+    a.warm = warm;
     a.pdas_cap = pdas_cap < RMPC_PDAS_ITERS ? pdas_cap : RMPC_PDAS_ITERS;
     const size_t lds = (size_t)dense_lds_doubles(N, bs, no) * sizeof(double);
     // one wave per SIMD (VGPR-bound): 4 per CU fill the chip, more only queue

@@ -222,7 +222,16 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         hist3 = hist2; hist2 = hist1; hist1 = hist0; hist0 = sig;
     }
     if (!cert || !isfinite(J)) {
-        a.retry[atomicAdd(a.retry_count, 1)] = (int32_t)b;    // generic kernel takes over
+        const int slot = atomicAdd(a.retry_count, 1);        // the next stage takes over
+        a.retry[slot] = (int32_t)b;
+        if (a.retry_sets) {                                   // ... from this active set
+            uint32_t *ws = a.retry_sets + (size_t)slot * (N + NB + 1);
+#pragma unroll
+            for (int k = 0; k < N; k++) ws[k] = Hf[k];
+#pragma unroll
+            for (int j = 0; j < NB; j++) ws[N + j] = Bf[j];
+            ws[N + NB] = (uint32_t)it;
+        }
         return;
     }
 #pragma unroll

@@ -3,6 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 tag=${1:-q}; shift
 for v in "$@"; do
+  [ "$v" = "-" ] && v=""
   echo "== $v"
   env $v timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/${tag}_bench.json 2>gpurun_out/${tag}_bench.err || exit $?
   python -c "import json;d=json.load(open('gpurun_out/${tag}_bench.json'));print('value %.3e ms/step %.3f'%(d['value'],d['ms_per_step']), d['solver'])"
