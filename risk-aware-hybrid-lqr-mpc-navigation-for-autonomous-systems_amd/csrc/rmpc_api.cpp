@@ -302,6 +302,16 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             HIP_TRY(c->retry_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
             a.retry_sets = (uint32_t *)c->retry_sets.p;
         }
+        // RMPC_DENSE_PROF=1: per-phase cycle counters of the fast and dense kernels to
+        // stderr (synchronises the stream; diagnostics only)
+        const bool prof = getenv("RMPC_DENSE_PROF") != nullptr;
+        unsigned long long *pc = nullptr;
+        if (prof) {
+            HIP_TRY(c->prof.ensure(64 * sizeof(unsigned long long)));
+            pc = (unsigned long long *)c->prof.p;
+            HIP_TRY(hipMemsetAsync(pc, 0, 64 * sizeof(unsigned long long), s));
+        }
+        a.prof = pc;
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[0], s));
         HIP_TRY(rmpc_launch_mpc_fast_f64(a, p->horizon, bs, s));
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[1], s));
@@ -311,15 +321,6 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         if (rmpc_mpc_dense_supported(p->horizon, bs, n_obs) && !getenv("RMPC_DISABLE_DENSE")) {
             HIP_TRY(c->retry2.ensure((size_t)B * sizeof(int32_t)));
             int32_t *cnt2 = (int32_t *)c->retry_count.p + 8;
-            // RMPC_DENSE_PROF=1: per-phase cycle counters of the dense kernel to stderr
-            // (synchronises the stream; diagnostics only)
-            const bool prof = getenv("RMPC_DENSE_PROF") != nullptr;
-            unsigned long long *pc = nullptr;
-            if (prof) {
-                HIP_TRY(c->prof.ensure(64 * sizeof(unsigned long long)));
-                pc = (unsigned long long *)c->prof.p;
-                HIP_TRY(hipMemsetAsync(pc, 0, 64 * sizeof(unsigned long long), s));
-            }
             HIP_TRY(rmpc_launch_mpc_dense_f64(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs,
                                               uref_rows, obstacles, step_count, u0, u_seq, x_pred, cost,
                                               status, slack_used, iters, left, left_n,
@@ -340,6 +341,10 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                         cn[0], cn[8], h[10], h[8], h[9], h[0] / r, h[1] / r, h[2] / r, h[3] / r, h[4] / r,
                         h[5] / r, h[6] / r, h[3] / (double)(h[8] ? h[8] : 1), h[4] / (double)(h[8] ? h[8] : 1),
                         (double)h[11] / r, (double)h[12] / r, (double)h[13] / r);
+                const double w = h[20] ? (double)h[20] : 1.0;
+                fprintf(stderr, "[fast] waves=%llu per wave: total %.0f back %.0f fwd %.0f iters %.2f | per iter: back %.0f fwd %.0f\n",
+                        h[20], h[19] / w, h[16] / w, h[17] / w, h[18] / w, h[16] / (double)(h[18] ? h[18] : 1),
+                        h[17] / (double)(h[18] ? h[18] : 1));
             }
             dbg_sync(s, "dense");
             left = (const int32_t *)c->retry2.p;

@@ -19,11 +19,43 @@
 
 namespace rmpc {
 
+// A per-wave tile of 16-byte rows (one row = 64 lanes x double2) addressed with buffer
+// instructions: the wave's base lives in one SGPR resource, the lane's byte offset in one
+// VGPR and the row offset is a constant SGPR offset -- so no per-row 64-bit address is
+// ever materialised (those got spilled, and a spill reload's vmcnt(0) wait defeated the
+// forward sweep's prefetch).
+struct WaveRows {
+    __amdgpu_buffer_rsrc_t r;
+    unsigned int vo;
+    __device__ __forceinline__ WaveRows(double2 *base, int rows, int lane)
+        : r(__builtin_amdgcn_make_buffer_rsrc(base, 0, rows * RMPC_WAVE * 16, 0x00020000)),
+          vo((unsigned int)lane * 16u) {}
+    __device__ __forceinline__ double2 ld(int row) const {
+        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+        const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, vo, row * RMPC_WAVE * 16, 0);
+        return __builtin_bit_cast(double2, v);
+    }
+    __device__ __forceinline__ void st(int row, double2 x) const {
+        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, x), r, vo, row * RMPC_WAVE * 16, 0);
+    }
+};
+
 template <int N, int BS>
 __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     constexpr int NB = (N + BS - 1) / BS;
     constexpr int PF = 4;     // gain blocks prefetched ahead in the forward sweep
     const int lane = threadIdx.x;
+    // Obstacles (x, y, d_safe + r) staged in LDS once: read from global inside the sweeps
+    // they compile to vector loads (the pointer may alias the kernel's stores) whose
+    // vmcnt(0) waits would drain the gain prefetch at every step.
+    __shared__ double obs_s[3 * RMPC_MAX_OBSTACLES];
+    if (lane < a.no) {
+        obs_s[3 * lane] = a.obs[3 * lane];
+        obs_s[3 * lane + 1] = a.obs[3 * lane + 1];
+        obs_s[3 * lane + 2] = a.prm.d_safe + a.obs[3 * lane + 2];
+    }
+    __syncthreads();
     const int64_t t = (int64_t)blockIdx.x * RMPC_WAVE + lane;
     const int64_t n = a.index ? (int64_t)*a.count : a.B;
     if (t >= n) return;
@@ -34,8 +66,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     const double Q0 = p.Q[0], Q1 = p.Q[1], Q2 = p.Q[2], R0 = p.R[0], R1 = p.R[1];
     const double *xr = a.x_refs + (size_t)b * a.ref_rows * 3;
     const double *ur = a.u_refs + (size_t)b * a.uref_rows * 2;
-    double2 *gt = a.gains + (size_t)blockIdx.x * NB * 4 * RMPC_WAVE + lane;
-    double2 *ut = a.usol + (size_t)blockIdx.x * NB * RMPC_WAVE + lane;
+    const WaveRows gt(a.gains + (size_t)blockIdx.x * NB * 4 * RMPC_WAVE, NB * 4, lane);
+    const WaveRows ut(a.usol + (size_t)blockIdx.x * NB * RMPC_WAVE, NB, lane);
 
     // ---- setup: np.unwrap'd reference heading, linearisation data (mpc_controller.py:391-428)
     // sin/cos of the heading and the reference speed stay in VGPRs; the reference position
@@ -77,6 +109,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     int it = 0, cert = 0, used = 0;
     double J = 0.0;
     const int maxit = min(p.max_iter, a.pdas_cap);
+    unsigned long long tp_b = 0, tp_f = 0, tp0 = a.prof ? __builtin_amdgcn_s_memtime() : 0ull;
+    const unsigned long long tp_setup = tp0;
     uint64_t hist0 = 0, hist1 = 0, hist2 = 0, hist3 = 0;   // active-set signatures (cycles)
     while (fin && it < maxit) {
         it++;
@@ -88,6 +122,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             asm volatile("" : "+v"(S[k]), "+v"(Cs[k]), "+v"(V0[k]));
         }
         // ---------------- backward block Riccati sweep
+        if (a.prof) tp0 = __builtin_amdgcn_s_memtime();
         RicV<double> V;
         V.P00 = p.P[0]; V.P01 = 0; V.P02 = 0; V.P11 = p.P[1]; V.P12 = 0; V.P22 = p.P[2];
         V.p0 = -p.P[0] * 0.0; V.p1 = -p.P[1] * 0.0; V.p2 = -p.P[2] * 0.0;
@@ -102,15 +137,15 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                 double q00 = Q0, q01 = 0, q11 = Q1;
                 double qv0 = -Q0 * 0.0, qv1 = -Q1 * 0.0, qv2 = -Q2 * 0.0;
                 if (k > 0 && Hf[k]) {
-                    for (int o = 0; o < no; o++) {
-                        if (!((Hf[k] >> o) & 1u)) continue;
+                    for (int o = 0; o < no; o++) {      // branch-free: inactive rows add 0
                         double n0, n1, hb;
-                        hinge_row_ltv(PX(k), PY(k), a.obs[3 * o], a.obs[3 * o + 1], p.d_safe + a.obs[3 * o + 2], n0, n1, hb);
-                        q00 += rho * n0 * n0;
-                        q01 += rho * n0 * n1;
-                        q11 += rho * n1 * n1;
-                        qv0 -= rho * hb * n0;
-                        qv1 -= rho * hb * n1;
+                        hinge_row_fast(PX(k), PY(k), obs_s[3 * o], obs_s[3 * o + 1], obs_s[3 * o + 2], n0, n1, hb);
+                        const double w = ((Hf[k] >> o) & 1u) ? rho : 0.0;
+                        q00 += w * n0 * n0;
+                        q01 += w * n0 * n1;
+                        q11 += w * n1 * n1;
+                        qv0 -= w * hb * n0;
+                        qv1 -= w * hb * n1;
                     }
                 }
                 const double vr = fabs(V0[k]) > 0.01 ? V0[k] : 0.1;     // :425
@@ -130,11 +165,16 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             const int bf0 = Bf[j] & 3, bf1 = (Bf[j] >> 2) & 3;
             double G[8];
             V = ric_block(W, bf0, bf1, bf0 == 1 ? lo0 : hi0, bf1 == 1 ? lo1 : hi1, G);
-            gt[(j * 4 + 0) * RMPC_WAVE] = make_double2(G[0], G[1]);
-            gt[(j * 4 + 1) * RMPC_WAVE] = make_double2(G[2], G[3]);
-            gt[(j * 4 + 2) * RMPC_WAVE] = make_double2(G[4], G[5]);
-            gt[(j * 4 + 3) * RMPC_WAVE] = make_double2(G[6], G[7]);
+            gt.st(j * 4 + 0, make_double2(G[0], G[1]));
+            gt.st(j * 4 + 1, make_double2(G[2], G[3]));
+            gt.st(j * 4 + 2, make_double2(G[4], G[5]));
+            gt.st(j * 4 + 3, make_double2(G[6], G[7]));
             __builtin_amdgcn_sched_barrier(0);
+        }
+        if (a.prof) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            tp_b += t1 - tp0;
+            tp0 = t1;
         }
         // ---------------- forward sweep + PDAS set update + objective
         // (opaque again: stops CSE from carrying backward-sweep values across this sweep)
@@ -149,12 +189,12 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
 #pragma unroll
         for (int j = 0; j < NB && j < PF; j++)
 #pragma unroll
-            for (int q = 0; q < 4; q++) g[j][q] = gt[(j * 4 + q) * RMPC_WAVE];
+            for (int q = 0; q < 4; q++) g[j][q] = gt.ld(j * 4 + q);
 #pragma unroll
         for (int j = 0; j < NB; j++) {
             if (j + PF < NB) {
 #pragma unroll
-                for (int q = 0; q < 4; q++) g[j + PF][q] = gt[((j + PF) * 4 + q) * RMPC_WAVE];
+                for (int q = 0; q < 4; q++) g[j + PF][q] = gt.ld((j + PF) * 4 + q);
             }
             const int k0 = j * BS;
             const int k1 = (k0 + BS < N) ? k0 + BS : N;
@@ -176,28 +216,25 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                 changed = 1;
                 Bf[j] = (uint32_t)(ns0 | (ns1 << 2));
             }
-            ut[j * RMPC_WAVE] = make_double2(u0v, u1v);
+            ut.st(j, make_double2(u0v, u1v));
 #pragma unroll
             for (int k = k0; k < k1; k++) {
                 J += Q0 * x0 * x0 + Q1 * x1 * x1 + Q2 * x2 * x2;
                 const double uu0 = u0v + V0[k], uu1 = u1v + V1(k);
                 J += R0 * uu0 * uu0 + R1 * uu1 * uu1;
                 uint32_t hk = Hf[k];
-                for (int o = 0; o < no; o++) {
+                for (int o = 0; o < no; o++) {          // branch-free row update
                     double n0, n1, hb;
-                    if (!hinge_row_ltv(PX(k), PY(k), a.obs[3 * o], a.obs[3 * o + 1], p.d_safe + a.obs[3 * o + 2], n0, n1, hb)) continue;
-                    const double r = hb - n0 * x0 - n1 * x1;
-                    if (r > 0) {
-                        J += rho * r * r;
-                        if (r > 1e-6) used = 1;                    // :485
-                    }
+                    const bool kept = hinge_row_fast(PX(k), PY(k), obs_s[3 * o], obs_s[3 * o + 1], obs_s[3 * o + 2], n0, n1, hb);
+                    const double r = kept ? hb - n0 * x0 - n1 * x1 : -1.0;   // unkept: never active
+                    const double rp = fmax(r, 0.0);
+                    J += rho * rp * rp;
+                    used |= (r > 1e-6);                                        // :485
                     if (k > 0) {
-                        const int act = (hk >> o) & 1u;
-                        const int na = act ? (r > -eps_h) : (r > eps_h);
-                        if (na != act) {
-                            changed = 1;
-                            hk ^= (1u << o);
-                        }
+                        const uint32_t act = (hk >> o) & 1u;
+                        const uint32_t na = act ? (r > -eps_h) : (r > eps_h);
+                        changed |= (int)(na != act);
+                        hk ^= (na ^ act) << o;
                     }
                 }
                 Hf[k] = hk;
@@ -210,6 +247,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             }
         }
         J += p.P[0] * x0 * x0 + p.P[1] * x1 * x1 + p.P[2] * x2 * x2;
+        if (a.prof) tp_f += __builtin_amdgcn_s_memtime() - tp0;
         if (!changed) { cert = 1; break; }
         // PDAS cycling: a repeated active-set signature hands the robot to the
         // projected-Newton phase of the generic kernel
@@ -220,6 +258,21 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         for (int j = 0; j < NB; j++) sig = (sig ^ (uint64_t)Bf[j]) * 1099511628211ull;
         if (sig == hist0 || sig == hist1 || sig == hist2 || sig == hist3) break;
         hist3 = hist2; hist2 = hist1; hist1 = hist0; hist0 = sig;
+    }
+    if (a.prof) {      // wave totals = max over lanes (the last lane saw every iteration)
+        unsigned long long mb = tp_b, mf = tp_f, mi = (unsigned long long)it;
+        for (int off = 32; off > 0; off >>= 1) {
+            mb = max(mb, (unsigned long long)__shfl_xor((long long)mb, off));
+            mf = max(mf, (unsigned long long)__shfl_xor((long long)mf, off));
+            mi = max(mi, (unsigned long long)__shfl_xor((long long)mi, off));
+        }
+        if (lane == 0) {
+            atomicAdd(a.prof + 16, mb);
+            atomicAdd(a.prof + 17, mf);
+            atomicAdd(a.prof + 18, mi);
+            atomicAdd(a.prof + 19, __builtin_amdgcn_s_memtime() - tp_setup);
+            atomicAdd(a.prof + 20, 1ull);
+        }
     }
     if (!cert || !isfinite(J)) {
         const int slot = atomicAdd(a.retry_count, 1);        // the next stage takes over
@@ -243,7 +296,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     double uc0 = 0, uc1 = 0;
 #pragma unroll
     for (int j = 0; j < NB; j++) {
-        const double2 u = ut[j * RMPC_WAVE];
+        const double2 u = ut.ld(j);
         const int k0 = j * BS;
         const int k1 = (k0 + BS < N) ? k0 + BS : N;
 #pragma unroll

@@ -167,6 +167,24 @@ __device__ __forceinline__ bool hinge_row_ltv(double px, double py, double ox, d
     return true;
 }
 
+// The same row, branch-free and without sqrt/division chains (for the register-resident
+// kernel, which re-derives every row in every sweep): 1/dist from v_rsq_f64 refined by one
+// Newton step (error ~1 ulp of the correctly rounded d/dist -- far below the 1e-9 parity
+// bar), `kept` as a predicate instead of a branch.
+__device__ __forceinline__ bool hinge_row_fast(double px, double py, double ox, double oy, double safe,
+                                               double &n0, double &n1, double &hb) {
+    const double ddx = px - ox, ddy = py - oy;
+    const double d2 = ddx * ddx + ddy * ddy;
+    double y = __builtin_amdgcn_rsq(d2);
+    const double hh = 0.5 * d2 * y;
+    y = fma(y, fma(-hh, y, 0.5), y);
+    const bool kept = d2 * y > 0.01;
+    n0 = ddx * y;
+    n1 = ddy * y;
+    hb = safe - (n0 * (px - ox) + n1 * (py - oy));
+    return kept;
+}
+
 // np.unwrap step (numpy 2.x): correction increment for consecutive samples prev -> th
 __device__ __forceinline__ double unwrap_step(double prev, double th) {
     const double dd = th - prev;
