@@ -325,7 +325,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                                               uref_rows, obstacles, step_count, u0, u_seq, x_pred, cost,
                                               status, slack_used, iters, left, left_n,
                                               (int32_t *)c->retry2.p, cnt2, (int32_t *)c->retry_count.p + 12,
-                                              getenv("RMPC_DENSE_CAP") ? atoi(getenv("RMPC_DENSE_CAP")) : 12,
+                                              getenv("RMPC_DENSE_CAP") ? atoi(getenv("RMPC_DENSE_CAP")) : 4,
                                               a.retry_sets, s, pc));
             if (prof) {
                 unsigned long long h[64];
@@ -337,10 +337,16 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                 fprintf(stderr,
                         "[dense] in=%d out=%d done=%llu iters(ph1)=%llu ph2=%llu | cycles/robot: stage %.0f "
                         "gam %.0f h0 %.0f solve %.0f test %.0f ph2 %.0f out %.0f | per ph1 iter: solve %.0f test %.0f"
-                        " | all solves: build %.0f chol %.0f subst %.0f\n",
+                        " | all solves: build %.0f (wz %.0f mfma %.0f rows %.0f) chol %.0f subst %.0f\n",
                         cn[0], cn[8], h[10], h[8], h[9], h[0] / r, h[1] / r, h[2] / r, h[3] / r, h[4] / r,
                         h[5] / r, h[6] / r, h[3] / (double)(h[8] ? h[8] : 1), h[4] / (double)(h[8] ? h[8] : 1),
+                        (double)(h[11] + h[14] + h[15]) / r, (double)h[14] / r, (double)h[15] / r,
                         (double)h[11] / r, (double)h[12] / r, (double)h[13] / r);
+                fprintf(stderr, "[dense] ph1 hist:");
+                for (int q = 0; q < 16; q++) fprintf(stderr, " %llu", h[24 + q]);
+                fprintf(stderr, " | ph2 hist:");
+                for (int q = 0; q < 16; q++) fprintf(stderr, " %llu", h[40 + q]);
+                fprintf(stderr, " | cycled %llu\n", h[56]);
                 const double w = h[20] ? (double)h[20] : 1.0;
                 fprintf(stderr, "[fast] waves=%llu per wave: total %.0f back %.0f fwd %.0f iters %.2f | per iter: back %.0f fwd %.0f\n",
                         h[20], h[19] / w, h[16] / w, h[17] / w, h[18] / w, h[16] / (double)(h[18] ? h[18] : 1),

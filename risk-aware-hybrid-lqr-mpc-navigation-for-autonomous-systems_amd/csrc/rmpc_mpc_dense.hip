@@ -384,6 +384,7 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
             }
         }
         __syncthreads();
+        DPROF(10);
         // M = H0 + Gam_pos' Z on the matrix cores (lower tiles), rows to MM
         {
             const int q = lane >> 4, c16 = lane & 15;
@@ -427,6 +428,7 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
                     }
         }
         __syncthreads();
+        DPROF(11);
         double m[n];
 #pragma unroll
         for (int l = 0; l < n; l++) m[l] = D::sym(d.MM, ic, l);
@@ -569,6 +571,7 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
     int it = 0, cert = 0;
     const int max_iter = p.max_iter;
     uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    int cyc = 0;
     while (it < max_iter && it < a.pdas_cap) {
         it++;
         solve();
@@ -584,7 +587,7 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
             const int w = __builtin_amdgcn_readlane(bf, 2 * j) | (__builtin_amdgcn_readlane(bf, 2 * j + 1) << 2);
             sig = (sig ^ (uint64_t)w) * 1099511628211ull;
         }
-        if (sig == s0 || sig == s1 || sig == s2 || sig == s3) break;
+        if (sig == s0 || sig == s1 || sig == s2 || sig == s3) { cyc = 1; break; }
         s3 = s2; s2 = s1; s1 = s0; s0 = sig;
     }
     const int it1 = it;
@@ -702,10 +705,15 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
     DPROF(6);
     if (prof_on && lane == 0) {
         for (int q = 0; q < 7; q++) atomicAdd(a.prof + q, pacc[q]);
-        for (int q = 7; q < 10; q++) atomicAdd(a.prof + 4 + q, pacc[q]);
+        for (int q = 7; q < 12; q++) atomicAdd(a.prof + 4 + q, pacc[q]);
         atomicAdd(a.prof + 8, (unsigned long long)it1);
         atomicAdd(a.prof + 9, (unsigned long long)(it > it1));
         atomicAdd(a.prof + 10, 1ull);
+        // histograms: phase-1 iterations (24 + it1, <= 15), phase-2 iterations (40 + .., <= 15),
+        // robots that left phase 1 on a detected cycle (56)
+        atomicAdd(a.prof + 24 + min(it1, 15), 1ull);
+        atomicAdd(a.prof + 40 + min(it - it1, 15), 1ull);
+        if (cyc) atomicAdd(a.prof + 56, 1ull);
     }
 }
 

@@ -164,7 +164,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             }
             const int bf0 = Bf[j] & 3, bf1 = (Bf[j] >> 2) & 3;
             double G[8];
-            V = ric_block(W, bf0, bf1, bf0 == 1 ? lo0 : hi0, bf1 == 1 ? lo1 : hi1, G);
+            V = ric_block_bf(W, bf0, bf1, bf0 == 1 ? lo0 : hi0, bf1 == 1 ? lo1 : hi1, G);
             gt.st(j * 4 + 0, make_double2(G[0], G[1]));
             gt.st(j * 4 + 1, make_double2(G[2], G[3]));
             gt.st(j * 4 + 2, make_double2(G[4], G[5]));

@@ -138,6 +138,57 @@ __device__ __forceinline__ RicV<T> ric_block(const RicW<T> &s, int bf0, int bf1,
     return v;
 }
 
+// Branch-free variant of ric_block for the register-resident kernel: the four free/fixed
+// cases as ONE masked 2x2 solve (a fixed component's row/column of Wuu becomes the
+// identity and its right-hand side the bound), and the determinant's reciprocal from
+// v_rcp_f64 + two Newton steps instead of a full IEEE division -- so a wave whose lanes
+// sit in different cases runs one path, not four.  Same outputs as ric_block up to
+// rounding.
+template <typename T>
+__device__ __forceinline__ RicV<T> ric_block_bf(const RicW<T> &s, int bf0, int bf1, T uc0, T uc1,
+                                                T G[8]) {
+    const bool fr0 = bf0 == 0, fr1 = bf1 == 0;
+    const T m00 = fr0 ? s.U00 : (T)1, m11 = fr1 ? s.U11 : (T)1;
+    const T m01 = (fr0 && fr1) ? s.U01 : (T)0;
+    const T det = m00 * m11 - m01 * m01;
+    T id = __builtin_amdgcn_rcp(det);
+    id = id * ((T)2 - det * id);
+    id = id * ((T)2 - det * id);
+    const T i00 = m11 * id, i01 = -m01 * id, i11 = m00 * id;
+    const T a0 = fr0 ? -s.X00 : (T)0, a1 = fr0 ? -s.X10 : (T)0, a2 = fr0 ? -s.X20 : (T)0;
+    const T b0 = fr1 ? -s.X01 : (T)0, b1 = fr1 ? -s.X11 : (T)0, b2 = fr1 ? -s.X21 : (T)0;
+    const T c0 = fr0 ? -(s.wu0 + (fr1 ? (T)0 : s.U01 * uc1)) : uc0;
+    const T c1 = fr1 ? -(s.wu1 + (fr0 ? (T)0 : s.U01 * uc0)) : uc1;
+    const T K00 = i00 * a0 + i01 * b0, K01 = i00 * a1 + i01 * b1, K02 = i00 * a2 + i01 * b2;
+    const T K10 = i01 * a0 + i11 * b0, K11 = i01 * a1 + i11 * b1, K12 = i01 * a2 + i11 * b2;
+    const T k0v = i00 * c0 + i01 * c1, k1v = i01 * c0 + i11 * c1;
+    const T MK00 = s.U00 * K00 + s.U01 * K10, MK01 = s.U00 * K01 + s.U01 * K11,
+            MK02 = s.U00 * K02 + s.U01 * K12;
+    const T MK10 = s.U01 * K00 + s.U11 * K10, MK11 = s.U01 * K01 + s.U11 * K11,
+            MK12 = s.U01 * K02 + s.U11 * K12;
+    const T Mk0 = s.U00 * k0v + s.U01 * k1v, Mk1 = s.U01 * k0v + s.U11 * k1v;
+    G[0] = fr0 ? K00 : (T)2 * (MK00 + s.X00);
+    G[1] = fr0 ? K01 : (T)2 * (MK01 + s.X10);
+    G[2] = fr0 ? K02 : (T)2 * (MK02 + s.X20);
+    G[3] = fr1 ? K10 : (T)2 * (MK10 + s.X01);
+    G[4] = fr1 ? K11 : (T)2 * (MK11 + s.X11);
+    G[5] = fr1 ? K12 : (T)2 * (MK12 + s.X21);
+    G[6] = fr0 ? k0v : (T)2 * (Mk0 + s.wu0);
+    G[7] = fr1 ? k1v : (T)2 * (Mk1 + s.wu1);
+    RicV<T> v;
+    v.P00 = s.W00 + (K00 * MK00 + K10 * MK10) + (T)2 * (s.X00 * K00 + s.X01 * K10);
+    v.P11 = s.W11 + (K01 * MK01 + K11 * MK11) + (T)2 * (s.X10 * K01 + s.X11 * K11);
+    v.P22 = s.W22 + (K02 * MK02 + K12 * MK12) + (T)2 * (s.X20 * K02 + s.X21 * K12);
+    v.P01 = s.W01 + (K00 * MK01 + K10 * MK11) + (s.X00 * K01 + s.X01 * K11) + (K00 * s.X10 + K10 * s.X11);
+    v.P02 = s.W02 + (K00 * MK02 + K10 * MK12) + (s.X00 * K02 + s.X01 * K12) + (K00 * s.X20 + K10 * s.X21);
+    v.P12 = s.W12 + (K01 * MK02 + K11 * MK12) + (s.X10 * K02 + s.X11 * K12) + (K01 * s.X20 + K11 * s.X21);
+    const T g0 = Mk0 + s.wu0, g1 = Mk1 + s.wu1;
+    v.p0 = s.wx0 + K00 * g0 + K10 * g1 + s.X00 * k0v + s.X01 * k1v;
+    v.p1 = s.wx1 + K01 * g0 + K11 * g1 + s.X10 * k0v + s.X11 * k1v;
+    v.p2 = s.wx2 + K02 * g0 + K12 * g1 + s.X20 * k0v + s.X21 * k1v;
+    return v;
+}
+
 // Forward: u (or, for fixed components, the bound) and multiplier e at state x; applies
 // the PDAS box rule.  Returns the new box state for component c.
 template <typename T>
