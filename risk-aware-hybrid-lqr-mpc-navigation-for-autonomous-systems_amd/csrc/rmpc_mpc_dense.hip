@@ -442,8 +442,7 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
         const uint64_t fixm = __ballot(lane < n && bf != 0);
         double r = -gi;
 #pragma unroll
-        for (int l = 0; l < n; l++)
-            if ((fixm >> l) & 1ull) r -= m[l] * rdl(fv, l);
+        for (int l = 0; l < n; l++) r -= m[l] * rdl(fv, l);      // free components: fv = 0
 #pragma unroll
         for (int l = 0; l < n; l++)
             if (((fixm >> l) & 1ull) || bf != 0) m[l] = (l == lane) ? 1.0 : 0.0;
@@ -458,9 +457,9 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
             const double piv = sqrt(dj), ip = 1.0 / piv;
             if (lane == j) { m[j] = piv; invd = ip; }
             else m[j] *= ip;
+            // (a fixed row k holds L_kj = 0 exactly, so its update is a no-op: no guard)
 #pragma unroll
-            for (int k = j + 1; k < n; k++)
-                if (!((fixm >> k) & 1ull)) m[k] -= m[j] * rdl(m[j], k);
+            for (int k = j + 1; k < n; k++) m[k] -= m[j] * rdl(m[j], k);
         }
         DPROF(8);
         // forward: L y = r
@@ -579,7 +578,9 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
         const int chg = pdas_test(0);
         DPROF(4);
         if (!chg) { cert = 1; break; }
-        // signature of (hinge flags, box states): the FNV walk of the other kernels
+        // signature of (hinge flags, box states): the FNV walk of the other kernels (a
+        // repeat needs >= 2 iterations after a first state, so short caps skip it)
+        if (a.pdas_cap <= 4) continue;
         uint64_t sig = 1469598103934665603ull;
         for (int k = 0; k < N; k++)
             sig = (sig ^ (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hf, k)) * 1099511628211ull;
