@@ -277,6 +277,8 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
     // (k, d) state components, K = 3N), and g0 = 2(Gam' W xf + E'R us) per lane
     {
         constexpr int NT = D::NT, NT16 = D::NT16, KS0 = (3 * N + 3) / 4;
+        const double q0w = p.Q[0], q1w = p.Q[1], q2w = p.Q[2], p0w = p.P[0], p1w = p.P[1], p2w = p.P[2];
+        const double r0w = p.R[0], r1w = p.R[1];
         dbl4 acc[NT * (NT + 1) / 2];
 #pragma unroll
         for (int t = 0; t < NT * (NT + 1) / 2; t++) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
@@ -286,7 +288,11 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
             const int kk = 4 * st + q;
             const bool valid = kk < 3 * N;
             const int k = 1 + (valid ? kk / 3 : 0), dd = valid ? kk % 3 : 0;
-            const double w = valid ? (k < N ? p.Q[dd] : p.P[dd]) : 0.0;
+            // (weights selected from scalars: a per-lane index into the kernel arguments
+            // would become a vector global load + vmcnt(0) in every k-step)
+            const double wq = dd == 0 ? q0w : (dd == 1 ? q1w : q2w);
+            const double wp = dd == 0 ? p0w : (dd == 1 ? p1w : p2w);
+            const double w = valid ? (k < N ? wq : wp) : 0.0;
             double av[NT], bv[NT];
 #pragma unroll
             for (int t = 0; t < NT; t++) {
@@ -314,7 +320,7 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
                             const int jb = row >> 1, cc = row & 1;
                             int cnt = 0;
                             for (int k = jb * BS; k < (jb + 1) * BS && k < N; k++) cnt++;
-                            v += p.R[cc] * cnt;
+                            v += (cc ? r1w : r0w) * cnt;
                         }
                         d.H0[row * NPL + col] = 2.0 * v;
                     }
@@ -323,19 +329,21 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
     double g0i = 0.0;
 #pragma unroll 2
     for (int k = 1; k <= N; k++) {
-        const double *Wd = k < N ? p.Q : p.P;
-        g0i += Wd[0] * d.G(k, 0, ic) * d.XF[3 * k] + Wd[1] * d.G(k, 1, ic) * d.XF[3 * k + 1] +
-               Wd[2] * d.G(k, 2, ic) * d.XF[3 * k + 2];
+        const bool term = k == N;
+        g0i += (term ? p.P[0] : p.Q[0]) * d.G(k, 0, ic) * d.XF[3 * k] +
+               (term ? p.P[1] : p.Q[1]) * d.G(k, 1, ic) * d.XF[3 * k + 1] +
+               (term ? p.P[2] : p.Q[2]) * d.G(k, 2, ic) * d.XF[3 * k + 2];
     }
     {
         const int j = ic >> 1, c = ic & 1;
         double us = 0;
         for (int k = j * BS; k < (j + 1) * BS && k < N; k++) us += ur[2 * k + c];
-        g0i = 2.0 * (g0i + p.R[c] * us);
+        g0i = 2.0 * (g0i + (c ? p.R[1] : p.R[0]) * us);
     }
     // the padded rows of the hinge product stay zero
     for (int e = lane; e < (4 * D::KS - 2 * N) * D::NT16; e += 64) d.ZM[2 * N * D::NT16 + e] = 0.0;
     __syncthreads();
+    DPROF(2);
 
     // ---- PDAS state: hinge flags of step k on lane k, box state of component i on lane i
     uint32_t hf = 0;
@@ -528,8 +536,9 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
         d.traj(dt, y0, y1, y2);
         double jl = 0.0;
         if (lane <= N) {
-            const double *Wd = lane < N ? p.Q : p.P;
-            jl = Wd[0] * y0 * y0 + Wd[1] * y1 * y1 + Wd[2] * y2 * y2;
+            const bool term = lane == N;      // (values, not a per-lane pointer: see H0)
+            jl = (term ? p.P[0] : p.Q[0]) * y0 * y0 + (term ? p.P[1] : p.Q[1]) * y1 * y1 +
+                 (term ? p.P[2] : p.Q[2]) * y2 * y2;
             if (lane < N) {
                 const int j = lane / BS;
                 const double uu0 = d.ZB[2 * j] + d.US0(lane), uu1 = d.ZB[2 * j + 1] + d.US1(lane);
@@ -651,8 +660,9 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
     double jl = 0.0;
     int used = 0;
     if (lane <= N) {
-        const double *Wd = lane < N ? p.Q : p.P;
-        jl = Wd[0] * y0 * y0 + Wd[1] * y1 * y1 + Wd[2] * y2 * y2;
+        const bool term = lane == N;
+        jl = (term ? p.P[0] : p.Q[0]) * y0 * y0 + (term ? p.P[1] : p.Q[1]) * y1 * y1 +
+             (term ? p.P[2] : p.Q[2]) * y2 * y2;
         if (lane < N) {
             const int j = lane / BS;
             const double uu0 = d.ZB[2 * j] + d.US0(lane), uu1 = d.ZB[2 * j + 1] + d.US1(lane);
