@@ -212,6 +212,43 @@ int rmpc_plant_step_batch(RmpcCtx *ctx, int64_t B, const double *x, const double
 int rmpc_figure8_batch(RmpcCtx *ctx, int64_t B, const double *t0, int32_t rows, double A,
                        double a, double dt, double *x_refs, double *u_refs);
 
+/* ---- closed-loop rollouts (run_simulation.py --mode lqr | mpc | hybrid) -------------------
+ * B independent robots tracking the Figure-8 reference TABLE of
+ * ReferenceTrajectoryGenerator.generate (row j at t = j*dt, table_len rows; indices past the
+ * end clamp to the last row as get_reference_at_index / get_trajectory_segment do,
+ * reference_generator.py:196-230, 277-326).  Robot b starts at table row start_index[b]
+ * (NULL = 0) from state x0[b] (NULL = the reference at that row, run_simulation.py:64-65).
+ * Step k, all on the device: references at rows start+k.., control -- LQR:
+ * compute_control_at_operating_point (:77-80); MPC: solve_with_ltv every mpc_rate steps with
+ * the control held in between (:243-259); hybrid: risk + dwell switch + branch (:525-559) --
+ * then DifferentialDriveRobot.simulate_step (differential_drive.py:138-172).
+ * Outputs (each nullable): states [B][steps+1][3], controls [B][steps][2], used_mpc
+ * [B][steps] (hybrid), mpc_status [4] = counts of MPC solve statuses over the rollout.
+ */
+typedef struct RmpcRolloutParams {
+    int32_t mode;          /* 0 LQR, 1 MPC, 2 hybrid                                    */
+    int32_t steps;         /* control steps                                             */
+    int32_t table_len;     /* rows of generate(duration) = len(np.arange(0, duration, dt)) */
+    int32_t mpc_rate;      /* MPC every mpc_rate steps (run_simulation.py:243, 5)       */
+    int32_t plant_method;  /* 0 euler, 1 rk4                                            */
+    int32_t _pad0;
+    double dt;             /* simulation / reference step                               */
+    double A, a;           /* Figure-8 amplitude and frequency (reference_generator.py) */
+    double v_max;          /* DifferentialDriveRobot limits (run_simulation.py:52)      */
+    double omega_max;
+} RmpcRolloutParams;
+
+int rmpc_rollout_batch(RmpcCtx *ctx, const RmpcRolloutParams *rp, const RmpcLqrParams *lp,
+                       const RmpcMpcParams *mp, const RmpcRiskParams *kp, int64_t B,
+                       const int32_t *start_index, const double *x0, const double *obstacles,
+                       int32_t n_obs, double *states, double *controls, uint8_t *used_mpc,
+                       int64_t *mpc_status);
+int rmpc_rollout_batch_dev(RmpcCtx *ctx, const RmpcRolloutParams *rp, const RmpcLqrParams *lp,
+                           const RmpcMpcParams *mp, const RmpcRiskParams *kp, int64_t B,
+                           const int32_t *start_index, const double *x0, const double *obstacles,
+                           int32_t n_obs, double *states, double *controls, uint8_t *used_mpc,
+                           int64_t *mpc_status, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

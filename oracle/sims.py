@@ -13,15 +13,14 @@ from .plant import simulate_step
 from .risk import RiskMetrics
 
 
-def lqr_closed_loop(duration=20.0, dt=0.02, Q=(15.0, 15.0, 8.0)):
+def lqr_closed_loop(duration=20.0, dt=0.02, Q=(15.0, 15.0, 8.0), steps=None, start=0, x0=None):
     g = Figure8(2.0, 0.5, dt)
     tab = g.generate(duration)
     c = LQRController(list(Q), [0.1, 0.1], dt, 2.0, 3.0)
-    x, _ = g.reference_at_index(0)
-    x = x.copy()
+    x = (g.reference_at_index(start)[0] if x0 is None else np.asarray(x0, float)).copy()
     st, ct = [x.copy()], []
-    for k in range(len(tab) - 1):
-        xr, ur = g.reference_at_index(k)
+    for k in range(len(tab) - 1 if steps is None else steps):
+        xr, ur = g.reference_at_index(start + k)
         u, _ = c.compute_control_at_operating_point(x, xr, ur)
         x = simulate_step(x, u, dt, 2.0, 3.0)
         st.append(x.copy())
@@ -30,7 +29,7 @@ def lqr_closed_loop(duration=20.0, dt=0.02, Q=(15.0, 15.0, 8.0)):
 
 
 def mpc_closed_loop(duration=20.0, dt=0.02, obstacles=None, steps=None, mpc_kwargs=None,
-                    mpc_rate=5):
+                    mpc_rate=5, start=0, x0=None):
     g = Figure8(2.0, 0.5, dt)
     tab = g.generate(duration)
     kw = dict(horizon=6, Q_diag=[15.0, 15.0, 50.0], R_diag=[0.1, 0.1],
@@ -39,13 +38,12 @@ def mpc_closed_loop(duration=20.0, dt=0.02, obstacles=None, steps=None, mpc_kwar
     kw.update(mpc_kwargs or {})
     c = MPCController(**kw)
     obstacles = default_obstacles() if obstacles is None else obstacles
-    x, _ = g.reference_at_index(0)
-    x = x.copy()
+    x = (g.reference_at_index(start)[0] if x0 is None else np.asarray(x0, float)).copy()
     n = len(tab) - 1 if steps is None else steps
     st, ct = [x.copy()], []
     sol = None
     for k in range(n):
-        xr, ur = g.segment(k, c.N + 1)
+        xr, ur = g.segment(start + k, c.N + 1)
         if k % mpc_rate == 0:
             sol = c.solve_with_ltv(x, xr, ur, obstacles)
         u = sol.optimal_control
@@ -56,7 +54,7 @@ def mpc_closed_loop(duration=20.0, dt=0.02, obstacles=None, steps=None, mpc_kwar
 
 
 def hybrid_closed_loop(duration=20.0, dt=0.02, obstacles=None, steps=None, mpc_kwargs=None,
-                       lqr_Q=(15.0, 15.0, 8.0)):
+                       lqr_Q=(15.0, 15.0, 8.0), start=0, x0=None):
     g = Figure8(2.0, 0.5, dt)
     tab = g.generate(duration)
     lq = LQRController(list(lqr_Q), [0.1, 0.1], dt, 2.0, 3.0)
@@ -68,13 +66,12 @@ def hybrid_closed_loop(duration=20.0, dt=0.02, obstacles=None, steps=None, mpc_k
     rm = RiskMetrics(d_safe=0.3, d_trigger=1.0, alpha=0.6, beta=0.4, threshold_low=0.2,
                      threshold_medium=0.5)
     obstacles = default_obstacles() if obstacles is None else obstacles
-    x, _ = g.reference_at_index(0)
-    x = x.copy()
+    x = (g.reference_at_index(start)[0] if x0 is None else np.asarray(x0, float)).copy()
     n = len(tab) - 1 if steps is None else steps
     prev, since = None, 0
     st, ct, used = [x.copy()], [], []
     for k in range(n):
-        xr, ur = g.reference_at_index(k)
+        xr, ur = g.reference_at_index(start + k)
         a = rm.assess(x, obstacles)
         if since >= 10:                                              # :533-537
             use_mpc = a["use_mpc"]
@@ -87,7 +84,7 @@ def hybrid_closed_loop(duration=20.0, dt=0.02, obstacles=None, steps=None, mpc_k
             since += 1
         prev = cur
         if use_mpc:
-            xs, us = g.segment(k, c.N + 1)
+            xs, us = g.segment(start + k, c.N + 1)
             u = c.solve_with_ltv(x, xs, us, obstacles).optimal_control
         else:
             u, _ = lq.compute_control_at_operating_point(x, xr, ur)

@@ -76,6 +76,9 @@ struct RmpcCtx {
     DevBuf stage[SB_COUNT];    // staging buffers for host-pointer entry points
     DevBuf idx_lqr, idx_mpc, counts, hyb_status;
     DevBuf fast_gains, fast_usol, retry, retry2, retry_count, prof, retry_sets;
+    // closed-loop rollout state (rmpc_rollout_batch)
+    DevBuf ro_x, ro_xr, ro_ur, ro_u, ro_step, ro_cache, ro_prev, ro_since, ro_status, ro_used,
+        ro_risk, ro_counts;
     // stage timing of the last MPC launch (rmpc_ctx_set_timing): events before/after
     // the lane-per-robot, wave-per-robot and generic stages
     bool timing = false;
@@ -132,6 +135,9 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
         if (e) (void)hipEventDestroy(e);
     c->retry2.release();
     c->retry_sets.release();
+    for (DevBuf *d : {&c->ro_x, &c->ro_xr, &c->ro_ur, &c->ro_u, &c->ro_step, &c->ro_cache, &c->ro_prev,
+                      &c->ro_since, &c->ro_status, &c->ro_used, &c->ro_risk, &c->ro_counts})
+        d->release();
     c->prof.release();
     c->retry_count.release();
     (void)hipStreamDestroy(c->stream);
@@ -681,6 +687,114 @@ extern "C" int rmpc_figure8_batch(RmpcCtx *c, int64_t B, const double *t0, int32
     HIP_TRY(rmpc_launch_figure8(B, dt0, rows, A, a, dt, dxr, dur, c->stream));
     RC(d2h(c, x_refs, dxr, (size_t)B * rows * 3));
     RC(d2h(c, u_refs, dur, (size_t)B * rows * 2));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RMPC_OK;
+}
+
+// ------------------------------------------------------------------------------ rollouts
+extern "C" int rmpc_rollout_batch_dev(RmpcCtx *c, const RmpcRolloutParams *rp, const RmpcLqrParams *lp,
+                                      const RmpcMpcParams *mp, const RmpcRiskParams *kp, int64_t B,
+                                      const int32_t *start_index, const double *x0, const double *obstacles,
+                                      int32_t n_obs, double *states, double *controls, uint8_t *used_mpc,
+                                      int64_t *mpc_status, void *stream) {
+    if (!c || !rp) return fail(RMPC_EINVAL, "ctx/params is NULL");
+    const int mode = rp->mode;
+    if (mode < 0 || mode > 2) return fail(RMPC_EINVAL, "mode must be 0 (LQR), 1 (MPC) or 2 (hybrid)");
+    if (rp->steps < 0 || rp->table_len < 1 || rp->mpc_rate < 1 || !(rp->dt > 0) ||
+        (rp->plant_method != 0 && rp->plant_method != 1))
+        return fail(RMPC_EINVAL, "bad rollout parameters");
+    if (mode != 1 && !lp) return fail(RMPC_EINVAL, "LQR params required");
+    if (mode != 0 && !mp) return fail(RMPC_EINVAL, "MPC params required");
+    if (mode == 2 && !kp) return fail(RMPC_EINVAL, "risk params required");
+    if (lp) RC(check_lqr(lp));
+    const int rows = mode == 0 ? 1 : mp->horizon + 1;
+    if (mode != 0) {
+        RC(check_mpc_params(mp, rows, rows, n_obs));
+        if (mp->formulation != RMPC_LTV) return fail(RMPC_EINVAL, "rollouts use solve_with_ltv (LTV)");
+    }
+    if (B < 0) return fail(RMPC_EINVAL, "B < 0");
+    if (B == 0) return RMPC_OK;
+    if (n_obs > 0 && !obstacles) return fail(RMPC_EINVAL, "obstacles is NULL");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = pick(c, stream);
+    HIP_TRY(c->ro_x.ensure((size_t)B * 3 * sizeof(double)));
+    HIP_TRY(c->ro_xr.ensure((size_t)B * rows * 3 * sizeof(double)));
+    HIP_TRY(c->ro_ur.ensure((size_t)B * rows * 2 * sizeof(double)));
+    HIP_TRY(c->ro_u.ensure((size_t)B * 2 * sizeof(double)));
+    HIP_TRY(c->ro_step.ensure((size_t)B * sizeof(int32_t)));
+    HIP_TRY(c->ro_cache.ensure((size_t)B * sizeof(RmpcLqrCache)));
+    HIP_TRY(c->ro_prev.ensure((size_t)B * sizeof(int32_t)));
+    HIP_TRY(c->ro_since.ensure((size_t)B * sizeof(int32_t)));
+    HIP_TRY(c->ro_status.ensure((size_t)B * sizeof(int32_t)));
+    HIP_TRY(c->ro_used.ensure((size_t)B));
+    HIP_TRY(c->ro_risk.ensure((size_t)B * sizeof(double)));
+    HIP_TRY(c->ro_counts.ensure(4 * sizeof(unsigned long long)));
+    double *x = (double *)c->ro_x.p, *xr = (double *)c->ro_xr.p, *ur = (double *)c->ro_ur.p;
+    double *u = (double *)c->ro_u.p;
+    int32_t *step = (int32_t *)c->ro_step.p, *prev = (int32_t *)c->ro_prev.p, *since = (int32_t *)c->ro_since.p;
+    int32_t *status = (int32_t *)c->ro_status.p;
+    RmpcLqrCache *cache = (RmpcLqrCache *)c->ro_cache.p;
+    uint8_t *used_now = (uint8_t *)c->ro_used.p;
+    unsigned long long *counts = (unsigned long long *)c->ro_counts.p;
+    HIP_TRY(hipMemsetAsync(counts, 0, 4 * sizeof(unsigned long long), s));
+    HIP_TRY(rmpc_launch_rollout_init(B, start_index, x0, rp->table_len, rp->A, rp->a, rp->dt, x, prev, since,
+                                     step, cache, states, rp->steps, s));
+    for (int k = 0; k < rp->steps; k++) {
+        HIP_TRY(rmpc_launch_figure8_table(B, start_index, k, rows, rp->table_len, rp->A, rp->a, rp->dt, xr, ur,
+                                          s));
+        if (mode == 0) {                                   // run_simulation.py:77-80
+            HIP_TRY(rmpc_launch_lqr_control(to_dev(lp), B, x, xr, 3, ur, 2, cache, u, nullptr, nullptr, nullptr,
+                                            nullptr, nullptr, nullptr, s));
+        } else if (mode == 1) {                            // :250-259, zero-order hold in u
+            if (k % rp->mpc_rate == 0) {
+                RC(launch_mpc(c, mp, B, x, xr, rows, ur, rows, obstacles, n_obs, step, u, nullptr, nullptr,
+                              nullptr, status, nullptr, nullptr, nullptr, nullptr, s));
+                HIP_TRY(rmpc_launch_status_count(B, status, nullptr, counts, s));
+            }
+        } else {                                           // :525-559
+            RC(rmpc_hybrid_step_batch_dev(c, kp, lp, mp, B, x, xr, rows, ur, rows, obstacles, n_obs, prev,
+                                          since, step, cache, u, used_now, (double *)c->ro_risk.p, s));
+            HIP_TRY(rmpc_launch_status_count(B, (const int32_t *)c->hyb_status.p, used_now, counts, s));
+        }
+        HIP_TRY(rmpc_launch_rollout_plant(B, x, u, rp->dt, rp->v_max, rp->omega_max, rp->plant_method, k,
+                                          rp->steps, states, controls, mode == 2 ? used_now : nullptr,
+                                          used_mpc, s));
+    }
+    if (mpc_status)
+        HIP_TRY(hipMemcpyAsync(mpc_status, counts, 4 * sizeof(unsigned long long), hipMemcpyDeviceToDevice, s));
+    return RMPC_OK;
+}
+
+extern "C" int rmpc_rollout_batch(RmpcCtx *c, const RmpcRolloutParams *rp, const RmpcLqrParams *lp,
+                                  const RmpcMpcParams *mp, const RmpcRiskParams *kp, int64_t B,
+                                  const int32_t *start_index, const double *x0, const double *obstacles,
+                                  int32_t n_obs, double *states, double *controls, uint8_t *used_mpc,
+                                  int64_t *mpc_status) {
+    if (!c || !rp) return fail(RMPC_EINVAL, "ctx/params is NULL");
+    if (B < 0 || rp->steps < 0) return fail(RMPC_EINVAL, "bad shape");
+    if (B == 0) return RMPC_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t K = (size_t)rp->steps;
+    int32_t *dstart;
+    double *dx0, *dobs = nullptr, *dst, *dct;
+    uint8_t *dused;
+    RC(h2d(c, SB_EXTRA1, start_index, (size_t)B, &dstart));
+    RC(h2d(c, SB_X0, x0, (size_t)B * 3, &dx0));
+    if (n_obs > 0) RC(h2d(c, SB_OBS, obstacles, (size_t)n_obs * 3, &dobs));
+    RC(dalloc(c, SB_XPRED, states, (size_t)B * (K + 1) * 3, &dst));
+    RC(dalloc(c, SB_USEQ, controls, (size_t)B * K * 2, &dct));
+    RC(dalloc(c, SB_SLACK, used_mpc, (size_t)B * K, &dused));
+    int64_t *dcnt = nullptr;
+    if (mpc_status) {
+        HIP_TRY(c->stage[SB_ITERS].ensure(64));
+        dcnt = (int64_t *)c->stage[SB_ITERS].p;
+    }
+    RC(rmpc_rollout_batch_dev(c, rp, lp, mp, kp, B, dstart, dx0, dobs, n_obs, dst, dct, dused, dcnt, c->stream));
+    RC(d2h(c, states, dst, (size_t)B * (K + 1) * 3));
+    RC(d2h(c, controls, dct, (size_t)B * K * 2));
+    RC(d2h(c, used_mpc, dused, (size_t)B * K));
+    if (mpc_status) RC(d2h(c, mpc_status, dcnt, (size_t)4));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RMPC_OK;
 }

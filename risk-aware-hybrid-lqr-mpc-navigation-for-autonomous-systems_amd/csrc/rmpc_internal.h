@@ -101,5 +101,18 @@ hipError_t rmpc_launch_hybrid_decide(const RiskDevParams &p, int64_t B, const do
                                      hipStream_t stream);
 hipError_t rmpc_launch_plant(int64_t B, const double *x, const double *u, double dt, double v_max,
                              double omega_max, int method, double *x_next, hipStream_t stream);
+hipError_t rmpc_launch_figure8_table(int64_t B, const int32_t *start, int32_t k, int rows, int32_t table_len,
+                                     double A, double a, double dt, double *x_refs, double *u_refs,
+                                     hipStream_t stream);
+hipError_t rmpc_launch_rollout_init(int64_t B, const int32_t *start, const double *x0, int32_t table_len,
+                                    double A, double a, double dt, double *x, int32_t *prev_ctrl,
+                                    int32_t *since, int32_t *step_count, RmpcLqrCache *cache, double *states,
+                                    int32_t steps, hipStream_t stream);
+hipError_t rmpc_launch_rollout_plant(int64_t B, double *x, const double *u, double dt, double v_max,
+                                     double omega_max, int method, int32_t k, int32_t steps, double *states,
+                                     double *controls, const uint8_t *used_now, uint8_t *used,
+                                     hipStream_t stream);
+hipError_t rmpc_launch_status_count(int64_t B, const int32_t *status, const uint8_t *mask,
+                                    unsigned long long *counts, hipStream_t stream);
 hipError_t rmpc_launch_figure8(int64_t B, const double *t0, int rows, double A, double a,
                                double dt, double *x_refs, double *u_refs, hipStream_t stream);

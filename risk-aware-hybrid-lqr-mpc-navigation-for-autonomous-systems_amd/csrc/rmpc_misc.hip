@@ -108,14 +108,10 @@ __global__ __launch_bounds__(256) void hybrid_decide_kernel(RiskDevParams p, int
     else idx_lqr[atomicAdd(&counts[0], 1)] = (int32_t)b;
 }
 
-// differential_drive.py:111-172
-__global__ __launch_bounds__(256) void plant_kernel(int64_t B, const double *x, const double *u, double dt,
-                                                    double v_max, double omega_max, int method,
-                                                    double *xn) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
-    const double v = clampv(u[2 * b], -v_max, v_max), w = clampv(u[2 * b + 1], -omega_max, omega_max);
-    const double x0 = x[3 * b], x1 = x[3 * b + 1], x2 = x[3 * b + 2];
+// differential_drive.py:111-172 (clip, Euler or RK4, while-wrap of theta)
+__device__ __forceinline__ void plant_step(double x0, double x1, double x2, double u0, double u1, double dt,
+                                           double v_max, double omega_max, int method, double *xn) {
+    const double v = clampv(u0, -v_max, v_max), w = clampv(u1, -omega_max, omega_max);
     double n0, n1, n2;
     if (method == 0) {
         n0 = x0 + dt * (v * cos(x2));
@@ -134,9 +130,18 @@ __global__ __launch_bounds__(256) void plant_kernel(int64_t B, const double *x, 
         n1 = x1 + h * (k11 + 2 * k21 + 2 * k31 + k41);
         n2 = x2 + h * (k12 + 2 * k22 + 2 * k32 + k42);
     }
-    xn[3 * b] = n0;
-    xn[3 * b + 1] = n1;
-    xn[3 * b + 2] = wrap_pi(n2);
+    xn[0] = n0;
+    xn[1] = n1;
+    xn[2] = wrap_pi(n2);
+}
+
+__global__ __launch_bounds__(256) void plant_kernel(int64_t B, const double *x, const double *u, double dt,
+                                                    double v_max, double omega_max, int method,
+                                                    double *xn) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    plant_step(x[3 * b], x[3 * b + 1], x[3 * b + 2], u[2 * b], u[2 * b + 1], dt, v_max, omega_max, method,
+               xn + 3 * b);
 }
 
 // reference_generator.py:86-172 evaluated at t0[b] + i*dt
@@ -147,24 +152,96 @@ __device__ __forceinline__ double heading8(double A, double a, double t) {
     return atan2(dpy, dpx);
 }
 
+// one reference point (px, py, theta, v, omega) at time t
+__device__ __forceinline__ void fig8_point(double A, double a, double dt, double t, double *xr, double *ur) {
+    const double s = sin(a * t), c = cos(a * t);
+    const double dpx = a * A * c, dpy = a * A * (c * c - s * s);
+    const double th = atan2(dpy, dpx);
+    xr[0] = A * s;
+    xr[1] = A * s * c;
+    xr[2] = th;
+    ur[0] = sqrt(dpx * dpx + dpy * dpy);
+    ur[1] = wrap_pi(heading8(A, a, t + dt) - th) / dt;       // :150-172 forward difference
+}
+
 __global__ __launch_bounds__(256) void figure8_kernel(int64_t B, const double *t0, int rows, double A, double a,
                                                       double dt, double *xr, double *ur) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= B * rows) return;
     const int64_t b = g / rows;
     const int i = (int)(g % rows);
-    const double t = t0[b] + (double)i * dt;
-    const double s = sin(a * t), c = cos(a * t);
-    const double px = A * s, py = A * s * c;
-    const double dpx = a * A * c, dpy = a * A * (c * c - s * s);
-    const double th = atan2(dpy, dpx);
-    const double v = sqrt(dpx * dpx + dpy * dpy);
-    const double om = wrap_pi(heading8(A, a, t + dt) - th) / dt;
-    xr[3 * g] = px;
-    xr[3 * g + 1] = py;
-    xr[3 * g + 2] = th;
-    ur[2 * g] = v;
-    ur[2 * g + 1] = om;
+    fig8_point(A, a, dt, t0[b] + (double)i * dt, xr + 3 * g, ur + 2 * g);
+}
+
+// Rows of the generate() table (t_j = j*dt exactly as np.arange) for table rows
+// start[b] + k + i, clamped to the last row (get_trajectory_segment :299-326)
+__global__ __launch_bounds__(256) void figure8_table_kernel(int64_t B, const int32_t *start, int32_t k, int rows,
+                                                            int32_t table_len, double A, double a, double dt,
+                                                            double *xr, double *ur) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= B * rows) return;
+    const int64_t b = g / rows;
+    const int i = (int)(g % rows);
+    int64_t j = (int64_t)(start ? start[b] : 0) + k + i;
+    if (j > table_len - 1) j = table_len - 1;
+    fig8_point(A, a, dt, (double)j * dt, xr + 3 * g, ur + 2 * g);
+}
+
+// rollout start: x = x0[b] or the reference at the start row; clear per-robot state
+__global__ __launch_bounds__(256) void rollout_init_kernel(int64_t B, const int32_t *start, const double *x0,
+                                                           int32_t table_len, double A, double a, double dt,
+                                                           double *x, int32_t *prev_ctrl, int32_t *since,
+                                                           int32_t *step_count, RmpcLqrCache *cache,
+                                                           double *states, int32_t steps) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    double xs[3], us[2];
+    if (x0) {
+        xs[0] = x0[3 * b]; xs[1] = x0[3 * b + 1]; xs[2] = x0[3 * b + 2];
+    } else {
+        int64_t j = start ? start[b] : 0;
+        if (j > table_len - 1) j = table_len - 1;
+        fig8_point(A, a, dt, (double)j * dt, xs, us);
+    }
+    x[3 * b] = xs[0]; x[3 * b + 1] = xs[1]; x[3 * b + 2] = xs[2];
+    prev_ctrl[b] = -1;
+    since[b] = 0;
+    step_count[b] = 0;
+    cache[b].valid = 0;
+    if (states) {
+        double *o = states + (size_t)b * (steps + 1) * 3;
+        o[0] = xs[0]; o[1] = xs[1]; o[2] = xs[2];
+    }
+}
+
+// plant step of a rollout, recording x_{k+1}, u_k (and the controller used)
+__global__ __launch_bounds__(256) void rollout_plant_kernel(int64_t B, double *x, const double *u, double dt,
+                                                            double v_max, double omega_max, int method, int32_t k,
+                                                            int32_t steps, double *states, double *controls,
+                                                            const uint8_t *used_now, uint8_t *used) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    double xn[3];
+    plant_step(x[3 * b], x[3 * b + 1], x[3 * b + 2], u[2 * b], u[2 * b + 1], dt, v_max, omega_max, method, xn);
+    x[3 * b] = xn[0]; x[3 * b + 1] = xn[1]; x[3 * b + 2] = xn[2];
+    if (states) {
+        double *o = states + ((size_t)b * (steps + 1) + k + 1) * 3;
+        o[0] = xn[0]; o[1] = xn[1]; o[2] = xn[2];
+    }
+    if (controls) {
+        double *o = controls + ((size_t)b * steps + k) * 2;
+        o[0] = u[2 * b]; o[1] = u[2 * b + 1];
+    }
+    if (used && used_now) used[(size_t)b * steps + k] = used_now[b];
+}
+
+__global__ __launch_bounds__(256) void status_count_kernel(int64_t B, const int32_t *status, const uint8_t *mask,
+                                                           unsigned long long *counts) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    if (mask && !mask[b]) return;
+    const int s = status[b];
+    if (s >= 0 && s < 4) atomicAdd(counts + s, 1ull);
 }
 
 }  // namespace rmpc
@@ -198,6 +275,42 @@ hipError_t rmpc_launch_plant(int64_t B, const double *x, const double *u, double
     if (B <= 0) return hipSuccess;
     hipLaunchKernelGGL(plant_kernel, dim3(nblk(B, 256)), dim3(256), 0, stream, B, x, u, dt, v_max,
                        omega_max, method, x_next);
+    return hipGetLastError();
+}
+
+hipError_t rmpc_launch_figure8_table(int64_t B, const int32_t *start, int32_t k, int rows, int32_t table_len,
+                                     double A, double a, double dt, double *x_refs, double *u_refs,
+                                     hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(figure8_table_kernel, dim3(nblk(B * rows, 256)), dim3(256), 0, stream, B, start, k, rows,
+                       table_len, A, a, dt, x_refs, u_refs);
+    return hipGetLastError();
+}
+
+hipError_t rmpc_launch_rollout_init(int64_t B, const int32_t *start, const double *x0, int32_t table_len,
+                                    double A, double a, double dt, double *x, int32_t *prev_ctrl,
+                                    int32_t *since, int32_t *step_count, RmpcLqrCache *cache, double *states,
+                                    int32_t steps, hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(rollout_init_kernel, dim3(nblk(B, 256)), dim3(256), 0, stream, B, start, x0, table_len, A,
+                       a, dt, x, prev_ctrl, since, step_count, cache, states, steps);
+    return hipGetLastError();
+}
+
+hipError_t rmpc_launch_rollout_plant(int64_t B, double *x, const double *u, double dt, double v_max,
+                                     double omega_max, int method, int32_t k, int32_t steps, double *states,
+                                     double *controls, const uint8_t *used_now, uint8_t *used,
+                                     hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(rollout_plant_kernel, dim3(nblk(B, 256)), dim3(256), 0, stream, B, x, u, dt, v_max,
+                       omega_max, method, k, steps, states, controls, used_now, used);
+    return hipGetLastError();
+}
+
+hipError_t rmpc_launch_status_count(int64_t B, const int32_t *status, const uint8_t *mask,
+                                    unsigned long long *counts, hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(status_count_kernel, dim3(nblk(B, 256)), dim3(256), 0, stream, B, status, mask, counts);
     return hipGetLastError();
 }
 

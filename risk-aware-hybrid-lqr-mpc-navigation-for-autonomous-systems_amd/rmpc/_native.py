@@ -47,6 +47,13 @@ class RiskParams(C.Structure):
                 ("min_dwell_steps", C.c_int32), ("_pad0", C.c_int32)]
 
 
+class RolloutParams(C.Structure):
+    _fields_ = [("mode", C.c_int32), ("steps", C.c_int32), ("table_len", C.c_int32),
+                ("mpc_rate", C.c_int32), ("plant_method", C.c_int32), ("_pad0", C.c_int32),
+                ("dt", C.c_double), ("A", C.c_double), ("a", C.c_double), ("v_max", C.c_double),
+                ("omega_max", C.c_double)]
+
+
 class LqrCache(C.Structure):
     _fields_ = [("K", C.c_double * 6), ("last_v", C.c_double), ("last_theta", C.c_double),
                 ("valid", C.c_int32), ("_pad0", C.c_int32)]
@@ -87,6 +94,11 @@ _PROTOS = {
                                    _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "rmpc_plant_step_batch": [_vp, _i64, _vp, _vp, _d, _d, _d, _i32, _vp],
     "rmpc_figure8_batch": [_vp, _i64, _vp, _i32, _d, _d, _d, _vp, _vp],
+    "rmpc_rollout_batch": [_vp, C.POINTER(RolloutParams), C.POINTER(LqrParams), C.POINTER(MpcParams),
+                           C.POINTER(RiskParams), _i64, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp],
+    "rmpc_rollout_batch_dev": [_vp, C.POINTER(RolloutParams), C.POINTER(LqrParams),
+                               C.POINTER(MpcParams), C.POINTER(RiskParams), _i64, _vp, _vp, _vp,
+                               _i32, _vp, _vp, _vp, _vp, _vp],
 }
 
 _lib = None

@@ -210,3 +210,39 @@ def mpc_stage_times(device=0):
     out = (C.c_double * 3)()
     check(lib.rmpc_mpc_stage_times(nat.context(device), out), "rmpc_mpc_stage_times")
     return tuple(out)
+
+
+ROLLOUT_MODES = {"lqr": 0, "mpc": 1, "hybrid": 2}
+
+
+def rollout_batch(mode, steps, lparams=None, mparams=None, rparams=None, start_index=None, x0=None,
+                  obstacles=None, table_len=1000, mpc_rate=5, dt=0.02, A=2.0, a=0.5, v_max=2.0,
+                  omega_max=3.0, plant="euler", B=None, device=0):
+    """Closed-loop rollouts of run_simulation.py --mode lqr|mpc|hybrid for B robots, entirely on
+    the device (references, control, plant).  Robot b starts at table row start_index[b] from
+    x0[b] (default: the reference there).  Returns dict states [B,steps+1,3], controls
+    [B,steps,2], used_mpc [B,steps] (bool), mpc_status [4] (counts over all MPC solves)."""
+    lib = nat.load()
+    if start_index is not None:
+        start_index = np.ascontiguousarray(start_index, np.int32).reshape(-1)
+        B = start_index.shape[0]
+    if x0 is not None:
+        x0 = f64(x0).reshape(-1, 3)
+        B = x0.shape[0]
+    if B is None:
+        raise ValueError("B, start_index or x0 is required")
+    rp = nat.RolloutParams()
+    rp.mode, rp.steps, rp.table_len = ROLLOUT_MODES[mode], int(steps), int(table_len)
+    rp.mpc_rate, rp.plant_method = int(mpc_rate), {"euler": 0, "rk4": 1}[plant]
+    rp.dt, rp.A, rp.a, rp.v_max, rp.omega_max = dt, A, a, v_max, omega_max
+    obs = _obs(obstacles)
+    states = np.empty((B, steps + 1, 3))
+    controls = np.empty((B, steps, 2))
+    used = np.zeros((B, steps), np.uint8)
+    counts = np.zeros(4, np.int64)
+    ref = lambda p: C.byref(p) if p is not None else None  # noqa: E731
+    check(lib.rmpc_rollout_batch(nat.context(device), C.byref(rp), ref(lparams), ref(mparams),
+                                 ref(rparams), B, ptr(start_index), ptr(x0), ptr(obs), obs.shape[0],
+                                 ptr(states), ptr(controls), ptr(used), ptr(counts)),
+          "rmpc_rollout_batch")
+    return dict(states=states, controls=controls, used_mpc=used.astype(bool), mpc_status=counts)

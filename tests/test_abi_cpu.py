@@ -45,6 +45,8 @@ def test_struct_layout_matches_header(tmp_path):
                  sizeof(RmpcRiskParams), sizeof(RmpcLqrCache));
           printf("%zu %zu %zu %zu\\n", offsetof(RmpcMpcParams, Q), offsetof(RmpcMpcParams, dt),
                  offsetof(RmpcLqrParams, max_iter), offsetof(RmpcLqrCache, valid));
+          printf("%zu %zu %zu\\n", sizeof(RmpcRolloutParams), offsetof(RmpcRolloutParams, dt),
+                 offsetof(RmpcRolloutParams, omega_max));
           return 0; }}"""))
     exe = tmp_path / "probe"
     subprocess.run(["gcc", str(probe), "-o", str(exe)], check=True)
@@ -52,7 +54,8 @@ def test_struct_layout_matches_header(tmp_path):
     got = [int(v) for v in out]
     want = [C.sizeof(n.MpcParams), C.sizeof(n.LqrParams), C.sizeof(n.RiskParams),
             C.sizeof(n.LqrCache), n.MpcParams.Q.offset, n.MpcParams.dt.offset,
-            n.LqrParams.max_iter.offset, n.LqrCache.valid.offset]
+            n.LqrParams.max_iter.offset, n.LqrCache.valid.offset,
+            C.sizeof(n.RolloutParams), n.RolloutParams.dt.offset, n.RolloutParams.omega_max.offset]
     assert got == want
     assert n.LQR_CACHE_DTYPE.itemsize == C.sizeof(n.LqrCache)
 

@@ -319,3 +319,69 @@ def test_hybrid_step_batch_matches_oracle_loop(rm):
         np.testing.assert_allclose(u, np.tile(ct_o[k], (B, 1)), atol=1e-8, rtol=0)
         x = rm.batch.plant_step_batch(x, u, 0.02, 2.0, 3.0)
     np.testing.assert_allclose(x, np.tile(st_o[-1], (B, 1)), atol=1e-8)
+
+
+# --------------------------------------------------------------------------- closed-loop rollouts
+# rmpc_rollout_batch: references, control and plant stay on the device for the whole rollout
+# (SURVEY 8(f) rank 1); each robot is compared with the oracle's restatement of
+# run_simulation.py started at the same table row.
+
+@pytest.mark.gpu
+def test_rollout_lqr_matches_oracle_closed_loop(rm):
+    steps, starts = 400, [0, 137, 600]
+    lp = rm._native.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0)
+    x0 = np.array([[0.05, -0.03, 0.2]]) + np.array(
+        [figure8.Figure8(2.0, 0.5, 0.02).reference_at_time(s * 0.02)[0] for s in starts])
+    for xs in (None, x0):
+        out = rm.batch.rollout_batch("lqr", steps, lparams=lp, start_index=starts, x0=xs)
+        for b, s0 in enumerate(starts):
+            st_o, ct_o = sims.lqr_closed_loop(steps=steps, start=s0, x0=None if xs is None else xs[b])
+            np.testing.assert_allclose(out["states"][b], st_o, atol=1e-10, rtol=0)
+            np.testing.assert_allclose(out["controls"][b], ct_o, atol=1e-10, rtol=0)
+
+
+@pytest.mark.gpu
+def test_rollout_mpc_matches_oracle_closed_loop(rm):
+    """run_mpc_simulation's configuration (N=6, bs=2, mpc_rate=5, default obstacles)."""
+    steps, starts = 120, [0, 230, 610]
+    mp = rm._native.mpc_params(6, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                               0.02, block_size=2)
+    out = rm.batch.rollout_batch("mpc", steps, mparams=mp, start_index=starts,
+                                 obstacles=ompc.default_obstacles())
+    assert out["mpc_status"][0] == len(starts) * ((steps + 4) // 5)      # every solve optimal
+    for b, s0 in enumerate(starts):
+        st_o, ct_o = sims.mpc_closed_loop(steps=steps, start=s0)
+        np.testing.assert_allclose(out["controls"][b], ct_o, atol=1e-8, rtol=0)
+        np.testing.assert_allclose(out["states"][b], st_o, atol=1e-8, rtol=0)
+
+
+@pytest.mark.gpu
+def test_rollout_hybrid_matches_oracle_closed_loop(rm):
+    steps, starts = 150, [0, 400]
+    rp = rm._native.risk_params()
+    lp = rm._native.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0)
+    mp = rm._native.mpc_params(6, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                               0.02, block_size=1)
+    out = rm.batch.rollout_batch("hybrid", steps, lparams=lp, mparams=mp, rparams=rp,
+                                 start_index=starts, obstacles=ompc.default_obstacles())
+    for b, s0 in enumerate(starts):
+        st_o, ct_o, used_o = sims.hybrid_closed_loop(steps=steps, start=s0)
+        np.testing.assert_array_equal(out["used_mpc"][b], used_o)
+        np.testing.assert_allclose(out["controls"][b], ct_o, atol=1e-8, rtol=0)
+        np.testing.assert_allclose(out["states"][b], st_o, atol=1e-8, rtol=0)
+    assert out["mpc_status"][0] == out["used_mpc"].sum()
+
+
+@pytest.mark.gpu
+def test_rollout_batch_is_independent_per_robot(rm):
+    """A robot's rollout does not depend on the batch it is in (no cross-robot coupling)."""
+    lp = rm._native.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0)
+    mp = rm._native.mpc_params(20, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                               0.02, block_size=1)
+    rp = rm._native.risk_params()
+    starts = np.arange(0, 999, 7, dtype=np.int32)
+    big = rm.batch.rollout_batch("hybrid", 60, lparams=lp, mparams=mp, rparams=rp,
+                                 start_index=starts, obstacles=ompc.default_obstacles())
+    one = rm.batch.rollout_batch("hybrid", 60, lparams=lp, mparams=mp, rparams=rp,
+                                 start_index=starts[17:18], obstacles=ompc.default_obstacles())
+    np.testing.assert_array_equal(big["states"][17], one["states"][0])
