@@ -385,3 +385,30 @@ def test_rollout_batch_is_independent_per_robot(rm):
     one = rm.batch.rollout_batch("hybrid", 60, lparams=lp, mparams=mp, rparams=rp,
                                  start_index=starts[17:18], obstacles=ompc.default_obstacles())
     np.testing.assert_array_equal(big["states"][17], one["states"][0])
+
+
+@pytest.mark.gpu
+def test_simulation_drop_ins_match_logs_and_oracle(rm, golden, tmp_path):
+    """rmpc.simulation mirrors run_simulation.py: the LQR run reproduces the reference's logged
+    999-step closed loop; MPC / hybrid runs equal the oracle loops; CSV logs use
+    SimulationLogger's columns."""
+    import csv
+    g = golden("lqr_closed_loop.npz")
+    r = rm.simulation.run_lqr_simulation(log_dir=str(tmp_path))
+    np.testing.assert_allclose(r["states"], g["states"], atol=1e-9, rtol=0)
+    np.testing.assert_allclose(r["controls"], g["controls"], atol=1e-9, rtol=0)
+    with open(next(tmp_path.glob("states_lqr_sim_*.csv"))) as f:
+        rows = list(csv.reader(f))
+    assert rows[0] == ["timestep", "px", "py", "theta", "px_ref", "py_ref", "theta_ref", "error_px",
+                       "error_py", "error_theta", "error_norm"]
+    assert len(rows) == 1 + 999
+    m = rm.simulation.run_mpc_simulation(duration=3.0, robots=2, start_index=[0, 300])
+    for b, s0 in enumerate([0, 300]):
+        st_o, _ = sims.mpc_closed_loop(duration=3.0, start=s0,
+                                       steps=len(np.arange(0, 3.0, 0.02)) - 1)
+        np.testing.assert_allclose(m["states"][b], st_o, atol=1e-8, rtol=0)
+    h = rm.simulation.run_hybrid_simulation(duration=3.0)
+    st_o, _, used_o = sims.hybrid_closed_loop(duration=3.0)
+    np.testing.assert_allclose(h["states"], st_o, atol=1e-8, rtol=0)
+    assert list(h["controller_used"]) == ["MPC" if u else "LQR" for u in used_o]
+    assert h["mpc_steps"] + h["lqr_steps"] == len(used_o)
