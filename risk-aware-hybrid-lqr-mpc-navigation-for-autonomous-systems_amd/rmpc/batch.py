@@ -169,6 +169,23 @@ def hybrid_step_batch(rparams, lparams, mparams, x, x_refs, u_refs, obstacles, s
     return u, used.astype(bool), risk
 
 
+def hybrid_step_batch_dev(rparams, lparams, mparams, x, x_refs, u_refs, obstacles, state, u_out,
+                          used_out, risk_out, device=0, stream=None):
+    """Device-tensor variant of hybrid_step_batch (torch tensors on cuda:device; state holds
+    device tensors prev_ctrl, steps_since, step_count (int32) and cache (uint8 bytes of
+    LQR_CACHE_DTYPE records)); asynchronous on `stream`."""
+    lib = nat.load()
+    s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+    check(lib.rmpc_hybrid_step_batch_dev(nat.context(device), C.byref(rparams), C.byref(lparams),
+                                         C.byref(mparams), x.shape[0], ptr(x), ptr(x_refs),
+                                         x_refs.shape[1], ptr(u_refs), u_refs.shape[1],
+                                         ptr(obstacles), obstacles.shape[0],
+                                         ptr(state["prev_ctrl"]), ptr(state["steps_since"]),
+                                         ptr(state["step_count"]), ptr(state["cache"]),
+                                         ptr(u_out), ptr(used_out), ptr(risk_out), s),
+          "rmpc_hybrid_step_batch_dev")
+
+
 def new_hybrid_state(B):
     return dict(prev_ctrl=np.full(B, -1, np.int32), steps_since=np.zeros(B, np.int32),
                 step_count=np.zeros(B, np.int32), cache=np.zeros(B, nat.LQR_CACHE_DTYPE))
