@@ -192,7 +192,8 @@ static int check_mpc_params(const RmpcMpcParams *p, int ref_rows, int uref_rows,
     if (ref_rows < 1 || uref_rows < 1) return fail(RMPC_EINVAL, "empty reference arrays");
     if (!p->soft && n_obs > 0)
         return fail(RMPC_ENOTSUP, "use_soft_constraints=False with obstacles (hard half-spaces) is not supported yet");
-    if (p->precision != RMPC_F64) return fail(RMPC_ENOTSUP, "precision %d not supported yet", p->precision);
+    if (p->precision != RMPC_F64 && p->precision != RMPC_F32)
+        return fail(RMPC_EINVAL, "precision %d is neither RMPC_F64 nor RMPC_F32", p->precision);
     if (!(p->dt > 0) || !(p->slack_penalty >= 0) || !(p->R[0] > 0) || !(p->R[1] > 0))
         return fail(RMPC_EINVAL, "dt, R must be > 0 and slack_penalty >= 0");
     return RMPC_OK;
@@ -274,7 +275,11 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
     const MpcDevParams d = to_dev(p);
     const bool fast = p->formulation == RMPC_LTV && p->precision == RMPC_F64 &&
                       rmpc_mpc_fast_supported(p->horizon, bs) && !getenv("RMPC_DISABLE_FAST");
-    if (!fast)
+    if (p->precision == RMPC_F32)          // fp32 arithmetic: the generic kernel on a float record
+        HIP_TRY(rmpc_launch_mpc_f32(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
+                                    step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
+                                    c->ws.p, index, count, s));
+    else if (!fast)
         HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
                                     step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
                                     c->ws.p, index, count, s));

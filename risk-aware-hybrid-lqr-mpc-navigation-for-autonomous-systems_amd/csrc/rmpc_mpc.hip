@@ -21,6 +21,16 @@
 
 namespace rmpc {
 
+// Active-set tolerances per arithmetic: fp64 certifies to ~1e-14; fp32 (BASELINE config 4)
+// to its own rounding level, else rows sitting on their boundary flip on rounding noise.
+template <typename T> struct SetTol;
+template <> struct SetTol<double> {
+    static constexpr double hinge = 1e-14, box = 1e-13, pn = 1e-6;
+};
+template <> struct SetTol<float> {
+    static constexpr float hinge = 2e-6f, box = 1e-5f, pn = 1e-4f;
+};
+
 template <typename T>
 struct MpcArgs {
     MpcDevParams prm;
@@ -227,7 +237,7 @@ __device__ int riccati_pass(const MpcDevParams &p, const MpcLayout &L, const Wav
         for (int i = 0; i < 8; i++) w(L.K + i * nb + j) = G[i];
     }
     // ---- forward pass + set update
-    const T eps_h = (T)1e-14, eps_b = (T)1e-13;
+    const T eps_h = SetTol<T>::hinge, eps_b = SetTol<T>::box;
     int changed = 0;
     T x0s = x0[0], x1s = x0[1], x2s = x0[2];
     for (int j = 0; j < nb; j++) {
@@ -433,7 +443,7 @@ __global__ __launch_bounds__(256) void mpc_solve_kernel(MpcArgs<T> a) {
                     wmax = fmax(wmax, fabs(z0 - clampv(z0 - w(L.G0 + j), w(L.LO0 + j), w(L.HI0 + j))));
                     wmax = fmax(wmax, fabs(z1 - clampv(z1 - w(L.G1 + j), w(L.LO1 + j), w(L.HI1 + j))));
                 }
-                const T eps = fmin((T)1e-6, wmax);
+                const T eps = fmin(SetTol<T>::pn, wmax);
                 for (int k = 1; k < L.N; k++)
                     for (int o = 0; o < L.no; o++) {
                         const int idx = k * L.no + o;
@@ -594,14 +604,15 @@ int rmpc_mpc_lds_lanes(const MpcLayout &L) {
     return lanes;
 }
 
-hipError_t rmpc_launch_mpc_f64(const MpcDevParams &prm, const MpcLayout &L, int64_t B,
+template <typename T>
+static hipError_t launch_generic(const MpcDevParams &prm, const MpcLayout &L, int64_t B,
                                const double *x0, const double *x_refs, int ref_rows,
                                const double *u_refs, int uref_rows, const double *obstacles,
                                int n_obs, int32_t *step_count, double *u0, double *u_seq,
                                double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
                                int32_t *iters, void *ws, const int32_t *index,
                                const int32_t *count, hipStream_t stream, int lds_lanes) {
-    MpcArgs<double> a;
+    MpcArgs<T> a;
     a.prm = prm;
     a.L = L;
     a.B = B;
@@ -610,27 +621,52 @@ hipError_t rmpc_launch_mpc_f64(const MpcDevParams &prm, const MpcLayout &L, int6
     a.step_count = step_count;
     a.u0 = u0; a.u_seq = u_seq; a.x_pred = x_pred; a.cost = cost;
     a.status = status; a.iters = iters; a.slack_used = slack_used;
-    a.ws = (double *)ws;
+    a.ws = (T *)ws;
     a.index = index;
     a.count = count;
     if (B <= 0) return hipSuccess;
     if (lds_lanes > 0) {
-        const size_t lds = (size_t)L.REC * lds_lanes * sizeof(double);
+        const size_t lds = (size_t)L.REC * lds_lanes * sizeof(T);
         static bool attr_set = false;
         if (!attr_set) {
-            hipError_t e = hipFuncSetAttribute((const void *)mpc_solve_kernel<double, true>,
+            hipError_t e = hipFuncSetAttribute((const void *)mpc_solve_kernel<T, true>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (e != hipSuccess) return e;
             attr_set = true;
         }
         const int64_t blocks = (B + lds_lanes - 1) / lds_lanes;
-        hipLaunchKernelGGL((mpc_solve_kernel<double, true>), dim3((unsigned)blocks), dim3(lds_lanes), lds,
+        hipLaunchKernelGGL((mpc_solve_kernel<T, true>), dim3((unsigned)blocks), dim3(lds_lanes), lds,
                            stream, a);
     } else {
         const int threads = 256;
         const int64_t blocks = (B + threads - 1) / threads;
-        hipLaunchKernelGGL((mpc_solve_kernel<double, false>), dim3((unsigned)blocks), dim3(threads), 0,
+        hipLaunchKernelGGL((mpc_solve_kernel<T, false>), dim3((unsigned)blocks), dim3(threads), 0,
                            stream, a);
     }
     return hipGetLastError();
+}
+
+hipError_t rmpc_launch_mpc_f64(const MpcDevParams &prm, const MpcLayout &L, int64_t B,
+                               const double *x0, const double *x_refs, int ref_rows,
+                               const double *u_refs, int uref_rows, const double *obstacles,
+                               int n_obs, int32_t *step_count, double *u0, double *u_seq,
+                               double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
+                               int32_t *iters, void *ws, const int32_t *index,
+                               const int32_t *count, hipStream_t stream, int lds_lanes) {
+    return launch_generic<double>(prm, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
+                                  step_count, u0, u_seq, x_pred, cost, status, slack_used, iters, ws, index,
+                                  count, stream, lds_lanes);
+}
+
+// fp32 arithmetic (BASELINE config 4): same algorithm, float workspace; inputs/outputs stay fp64
+hipError_t rmpc_launch_mpc_f32(const MpcDevParams &prm, const MpcLayout &L, int64_t B,
+                               const double *x0, const double *x_refs, int ref_rows,
+                               const double *u_refs, int uref_rows, const double *obstacles,
+                               int n_obs, int32_t *step_count, double *u0, double *u_seq,
+                               double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
+                               int32_t *iters, void *ws, const int32_t *index,
+                               const int32_t *count, hipStream_t stream, int lds_lanes) {
+    return launch_generic<float>(prm, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
+                                 step_count, u0, u_seq, x_pred, cost, status, slack_used, iters, ws, index,
+                                 count, stream, lds_lanes);
 }

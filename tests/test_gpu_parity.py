@@ -412,3 +412,26 @@ def test_simulation_drop_ins_match_logs_and_oracle(rm, golden, tmp_path):
     np.testing.assert_allclose(h["states"], st_o, atol=1e-8, rtol=0)
     assert list(h["controller_used"]) == ["MPC" if u else "LQR" for u in used_o]
     assert h["mpc_steps"] + h["lqr_steps"] == len(used_o)
+
+
+@pytest.mark.gpu
+def test_mpc_fp32_config4_accuracy(rm, capsys):
+    """BASELINE config 4 arithmetic (fp32, N=30, 8 obstacles) against the fp64 C port on the
+    same inputs: the achieved control error is measured and reported ("report
+    achieved relative error honestly")."""
+    B, N = 2048, 30
+    t0 = (np.arange(B) / B) * (2 * np.pi / 0.5)
+    x0, xr, ur = _workload(N, B, 2, t0=t0)
+    obs = ompc.union8_obstacles()
+    p = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02,
+                              precision=1)
+    out = rm.batch.mpc_solve_batch(p, x0, xr, ur, obs)
+    cp = cpu.mpc_params(N, (15, 15, 50), (.1, .1), (30, 30, 40), 0.3, 5000., 2., 3., 0.02)
+    ref = cpu.mpc_solve_batch(cp, x0, xr, ur, obs, threads=8)
+    both = (out["status"] <= 1) & (ref["status"] == 0)
+    assert both.mean() >= 0.99
+    rel = np.abs(out["u0"] - ref["u0"]).max(axis=1) / np.maximum(1.0, np.abs(ref["u0"]).max(axis=1))
+    with capsys.disabled():
+        print(f"\n[fp32 cfg4] status ok {both.mean():.4f}; rel |du0|: median {np.median(rel[both]):.2e} "
+              f"p99 {np.percentile(rel[both], 99):.2e} max {rel[both].max():.2e}")
+    assert rel[both].max() <= 1e-4          # the north star's control-error bound
