@@ -64,7 +64,6 @@ __host__ __device__ constexpr int dense_n(int N, int bs) { return 2 * ((N + bs -
 __host__ __device__ constexpr int dense_nt16(int N, int bs) { return (dense_n(N, bs) + 15) / 16 * 16; }
 __host__ __device__ constexpr int dense_lds_doubles(int N, int bs, int no) {
     return (N + 1) * 3 * dense_nt16(N, bs)                     // GAM [(N+1)*3][NT16] (zero pad)
-           + 4 * ((2 * N + 3) / 4) * dense_nt16(N, bs)         // ZM  [4*KS][NT16] hinge-scaled rows
            + 2 * dense_n(N, bs) * (dense_n(N, bs) + 1)         // H0, MM [n][n+1] (MM doubles as LT)
            + dense_n(N, bs)                                    // ZB  [n]
            + 6 * N                                             // STG [6][N]
@@ -105,7 +104,7 @@ struct Dense {
 
     const int lane, no, ic;           // ic: this lane's column, clamped below n
     double *const s0;
-    double *GAM, *ZM, *H0, *MM, *LT, *ZB, *STG, *XF, *FB, *WV, *HR;
+    double *GAM, *H0, *MM, *LT, *ZB, *STG, *XF, *FB, *WV, *HR;
 
     __device__ Dense(double *s, int lane_, int no_)
         : lane(lane_), no(no_), ic(lane_ < n ? lane_ : n - 1), s0(s) { refresh(); }
@@ -116,8 +115,7 @@ struct Dense {
         int o = 0;
         asm volatile("" : "+v"(o));
         GAM = s0 + o;
-        ZM = GAM + (N + 1) * 3 * NT16;
-        H0 = ZM + 4 * KS * NT16;
+        H0 = GAM + (N + 1) * 3 * NT16;
         MM = H0 + n * NPL;
         LT = MM;                      // the factor reuses the assembled matrix's space
         ZB = MM + n * NPL;
@@ -340,8 +338,6 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
         for (int k = j * BS; k < (j + 1) * BS && k < N; k++) us += ur[2 * k + c];
         g0i = 2.0 * (g0i + (c ? p.R[1] : p.R[0]) * us);
     }
-    // the padded rows of the hinge product stay zero
-    for (int e = lane; e < (4 * D::KS - 2 * N) * D::NT16; e += 64) d.ZM[2 * N * D::NT16 + e] = 0.0;
     __syncthreads();
     DPROF(2);
 
@@ -381,18 +377,6 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
             d.WV[3 * N + lane] = v0; d.WV[4 * N + lane] = v1;
         }
         __syncthreads();
-        // Z = blockdiag(W_k) Gam_pos (lane = column)
-        if (lane < NT16) {
-#pragma unroll 4
-            for (int k = 0; k < N; k++) {
-                const double gx = d.G(k, 0, lane), gy = d.G(k, 1, lane);
-                const double w00 = d.WV[k], w01 = d.WV[N + k], w11 = d.WV[2 * N + k];
-                d.ZM[(2 * k) * NT16 + lane] = w00 * gx + w01 * gy;
-                d.ZM[(2 * k + 1) * NT16 + lane] = w01 * gx + w11 * gy;
-            }
-        }
-        __syncthreads();
-        DPROF(10);
         // M = H0 + Gam_pos' Z on the matrix cores (lower tiles), rows to MM
         {
             const int q = lane >> 4, c16 = lane & 15;
@@ -409,13 +393,20 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
                     }
 #pragma unroll 2
             for (int st = 0; st < KS; st++) {
-                const int kk = 4 * st + q;                 // row (k, comp) = (kk >> 1, kk & 1)
-                const int grow = 3 * (kk >> 1) + (kk & 1);
+                // row (k, comp) = (kk >> 1, kk & 1) of Gam_pos; the B operand is the same row of
+                // Z = W_k Gam_pos,k formed on the fly (rows past step N-1 carry W = 0)
+                const int kk = 4 * st + q;
+                const int kz = kk >> 1, cz = kk & 1;
+                const bool live = kz < N;
+                const double w0 = live ? (cz ? d.WV[N + kz] : d.WV[kz]) : 0.0;        // w00 | w01
+                const double w1 = live ? (cz ? d.WV[2 * N + kz] : d.WV[N + kz]) : 0.0; // w01 | w11
                 double av[NT], bv[NT];
 #pragma unroll
                 for (int t = 0; t < NT; t++) {
-                    av[t] = d.GAM[grow * NT16 + 16 * t + c16];
-                    bv[t] = d.ZM[kk * NT16 + 16 * t + c16];
+                    const double gx = d.GAM[(3 * kz) * NT16 + 16 * t + c16];
+                    const double gy = d.GAM[(3 * kz + 1) * NT16 + 16 * t + c16];
+                    av[t] = cz ? gy : gx;
+                    bv[t] = w0 * gx + w1 * gy;
                 }
                 tt = 0;
 #pragma unroll
@@ -455,27 +446,23 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
         for (int l = 0; l < n; l++)
             if (((fixm >> l) & 1ull) || bf != 0) m[l] = (l == lane) ? 1.0 : 0.0;
         if (bf != 0) r = fv;
-        // right-looking Cholesky: lane i keeps L[i][0..i] in m (upper part: don't care)
-        // (a fixed component's column is e_j: nothing to eliminate, pivot 1)
+        // right-looking Cholesky, lane i keeps L[i][0..i] in m (upper part: don't care), with the
+        // forward substitution L y = r folded into the column loop: once column j is final,
+        // y_j = r_j / L_jj and every row below subtracts L_ij y_j.
+        // (a fixed component's column is e_j: nothing to eliminate, pivot 1, y_j = r_j)
         double invd = 1.0;
 #pragma unroll
         for (int j = 0; j < n; j++) {
-            if ((fixm >> j) & 1ull) continue;
+            if ((fixm >> j) & 1ull) continue;      // column e_j: y_j = r_j, rows below unchanged
             const double dj = rdl(m[j], j);
             const double piv = sqrt(dj), ip = 1.0 / piv;
-            if (lane == j) { m[j] = piv; invd = ip; }
+            if (lane == j) { m[j] = piv; invd = ip; r *= ip; }
             else m[j] *= ip;
+            const double yj = rdl(r, j);
+            if (lane > j) r -= m[j] * yj;
             // (a fixed row k holds L_kj = 0 exactly, so its update is a no-op: no guard)
 #pragma unroll
             for (int k = j + 1; k < n; k++) m[k] -= m[j] * rdl(m[j], k);
-        }
-        DPROF(8);
-        // forward: L y = r
-#pragma unroll
-        for (int j = 0; j < n; j++) {
-            const double yj = rdl(r * invd, j);
-            if (lane == j) r = yj;
-            else if (lane > j) r -= m[j] * yj;
         }
         // backward: L' z = y (rows of L through LDS, read column-wise)
         if (lane < n) {
@@ -625,10 +612,8 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
             it++;
             solve();
             if (!pdas_test(1)) { cert = 1; break; }
-            // Armijo along the projection arc
-            if (lane < n) d.ZB[lane] = z;
-            __syncthreads();
-            const double gz = true_grad();
+            // Armijo along the projection arc (the gradient at z is g from the loop top)
+            const double gz = g;
             double Ft = F, zt = z, alpha = 1.0;
             int acc = 0;
             for (int ls = 0; ls < 40; ls++) {
