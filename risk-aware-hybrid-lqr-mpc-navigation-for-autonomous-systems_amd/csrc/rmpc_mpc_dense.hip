@@ -455,7 +455,12 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
         for (int j = 0; j < n; j++) {
             if ((fixm >> j) & 1ull) continue;      // column e_j: y_j = r_j, rows below unchanged
             const double dj = rdl(m[j], j);
-            const double piv = sqrt(dj), ip = 1.0 / piv;
+            // 1/sqrt(d) from v_rsq_f64 + two Newton steps: a far shorter dependent chain than
+            // IEEE sqrt followed by a division, on the column loop's critical path
+            double ip = __builtin_amdgcn_rsq(dj);
+            ip = ip * (1.5 - 0.5 * dj * ip * ip);
+            ip = ip * (1.5 - 0.5 * dj * ip * ip);
+            const double piv = dj * ip;
             if (lane == j) { m[j] = piv; invd = ip; r *= ip; }
             else m[j] *= ip;
             const double yj = rdl(r, j);
