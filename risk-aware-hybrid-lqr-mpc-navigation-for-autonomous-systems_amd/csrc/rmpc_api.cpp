@@ -273,9 +273,10 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
     const MpcLayout L = rmpc_mpc_layout(p->horizon, bs, n_obs);
     HIP_TRY(ensure_ws(c, L, B));
     const MpcDevParams d = to_dev(p);
-    const bool fast = p->formulation == RMPC_LTV && p->precision == RMPC_F64 &&
-                      rmpc_mpc_fast_supported(p->horizon, bs) && !getenv("RMPC_DISABLE_FAST");
-    if (p->precision == RMPC_F32)          // fp32 arithmetic: the generic kernel on a float record
+    const bool f32 = p->precision == RMPC_F32;
+    const bool fast = p->formulation == RMPC_LTV && rmpc_mpc_fast_supported(p->horizon, bs, p->precision) &&
+                      !getenv("RMPC_DISABLE_FAST");
+    if (!fast && f32)                      // fp32 arithmetic: the generic kernel on a float record
         HIP_TRY(rmpc_launch_mpc_f32(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
                                     step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
                                     c->ws.p, index, count, s));
@@ -307,7 +308,9 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         a.count = count;
         a.retry = (int32_t *)c->retry.p;
         a.retry_count = (int32_t *)c->retry_count.p;
-        a.pdas_cap = getenv("RMPC_FAST_CAP") ? atoi(getenv("RMPC_FAST_CAP")) : 10;
+        // default cap: 10 at N <= 20 (tuned on BASELINE config 3), 16 beyond (config 4, where a
+        // dense-tail iteration at n = 60 costs ~2x a lane-per-robot one)
+        a.pdas_cap = getenv("RMPC_FAST_CAP") ? atoi(getenv("RMPC_FAST_CAP")) : (p->horizon <= 20 ? 10 : 16);
         const bool warm = !getenv("RMPC_COLD_TAIL");
         if (warm) {
             HIP_TRY(c->retry_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
@@ -324,7 +327,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         }
         a.prof = pc;
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[0], s));
-        HIP_TRY(rmpc_launch_mpc_fast_f64(a, p->horizon, bs, s));
+        HIP_TRY(rmpc_launch_mpc_fast(a, p->horizon, bs, p->precision, s));
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[1], s));
         dbg_sync(s, "fast");
         const int32_t *left = (const int32_t *)c->retry.p;
@@ -368,10 +371,16 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             left_n = cnt2;
         }
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[2], s));
-        // what remains is rare (cycling beyond both, non-finite data): LDS generic kernel
-        HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
-                                    step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
-                                    c->ws.p, left, left_n, s, rmpc_mpc_lds_lanes(L)));
+        // what remains is rare (cycling beyond both, non-finite data): LDS generic kernel, in
+        // the requested arithmetic (the dense tail between is fp64 for both)
+        if (f32)
+            HIP_TRY(rmpc_launch_mpc_f32(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
+                                        step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
+                                        c->ws.p, left, left_n, s, rmpc_mpc_lds_lanes(L)));
+        else
+            HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
+                                        step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
+                                        c->ws.p, left, left_n, s, rmpc_mpc_lds_lanes(L)));
         if (c->timing) {
             HIP_TRY(hipEventRecord(c->ev[3], s));
             c->timed = true;

@@ -21,16 +21,6 @@
 
 namespace rmpc {
 
-// Active-set tolerances per arithmetic: fp64 certifies to ~1e-14; fp32 (BASELINE config 4)
-// to its own rounding level, else rows sitting on their boundary flip on rounding noise.
-template <typename T> struct SetTol;
-template <> struct SetTol<double> {
-    static constexpr double hinge = 1e-14, box = 1e-13, pn = 1e-6;
-};
-template <> struct SetTol<float> {
-    static constexpr float hinge = 2e-6f, box = 1e-5f, pn = 1e-4f;
-};
-
 template <typename T>
 struct MpcArgs {
     MpcDevParams prm;

@@ -737,7 +737,7 @@ __global__ __launch_bounds__(64, 1) void mpc_dense_kernel(DenseArgs a) {
 using namespace rmpc;
 
 bool rmpc_mpc_dense_supported(int N, int bs, int no) {
-    const bool inst = (bs == 1 && (N == 6 || N == 10 || N == 20)) || (bs == 2 && N == 6);
+    const bool inst = (bs == 1 && (N == 6 || N == 10 || N == 20 || N == 30)) || (bs == 2 && N == 6);
     return inst && no <= 16 && (size_t)dense_lds_doubles(N, bs, no) * sizeof(double) <= 160 * 1024;
 }
 
@@ -770,7 +770,8 @@ hipError_t rmpc_launch_mpc_dense_f64(const MpcDevParams &prm, int N, int bs, int
     const int64_t gmax = (int64_t)256 * (per_cu > 0 ? per_cu : 4);
     const int64_t grid = capacity < gmax ? capacity : gmax;
     const dim3 g((unsigned)grid), blk(64);
-    const void *fn = (bs == 1 && N == 20)   ? (const void *)mpc_dense_kernel<20, 1>
+    const void *fn = (bs == 1 && N == 30)   ? (const void *)mpc_dense_kernel<30, 1>
+                     : (bs == 1 && N == 20) ? (const void *)mpc_dense_kernel<20, 1>
                      : (bs == 1 && N == 10) ? (const void *)mpc_dense_kernel<10, 1>
                      : (bs == 1 && N == 6)  ? (const void *)mpc_dense_kernel<6, 1>
                                             : (const void *)mpc_dense_kernel<6, 2>;
@@ -778,7 +779,8 @@ hipError_t rmpc_launch_mpc_dense_f64(const MpcDevParams &prm, int N, int bs, int
         const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_dense_kernel<20, 1>), g, blk, lds, stream, a);
+    if (bs == 1 && N == 30) hipLaunchKernelGGL((mpc_dense_kernel<30, 1>), g, blk, lds, stream, a);
+    else if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_dense_kernel<20, 1>), g, blk, lds, stream, a);
     else if (bs == 1 && N == 10) hipLaunchKernelGGL((mpc_dense_kernel<10, 1>), g, blk, lds, stream, a);
     else if (bs == 1 && N == 6) hipLaunchKernelGGL((mpc_dense_kernel<6, 1>), g, blk, lds, stream, a);
     else hipLaunchKernelGGL((mpc_dense_kernel<6, 2>), g, blk, lds, stream, a);

@@ -9,6 +9,10 @@
 // with the forward sweep prefetching PF blocks ahead.  Obstacle rows are recomputed from
 // registers on every pass instead of being streamed.
 //
+// Templated on the arithmetic type T: double for the fp64 configurations; float for fp32
+// requests (BASELINE config 4: N=30, 8 obstacles), where the register-resident layout would
+// not fit in fp64 at that horizon.  Inputs and outputs stay fp64 in both.
+//
 // One wave per workgroup, one lane per robot.  A robot that is not certified within the
 // PDAS phase (cycling, ~1e-4 of instances) or has non-finite data is appended to a retry
 // list that the generic kernel (projected-Newton phase, fallback law) consumes next on
@@ -24,36 +28,109 @@ namespace rmpc {
 // VGPR and the row offset is a constant SGPR offset -- so no per-row 64-bit address is
 // ever materialised (those got spilled, and a spill reload's vmcnt(0) wait defeated the
 // forward sweep's prefetch).
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+
+template <int RB>      // bytes per lane and row: 16 or 8
 struct WaveRows {
     __amdgpu_buffer_rsrc_t r;
     unsigned int vo;
-    __device__ __forceinline__ WaveRows(double2 *base, int rows, int lane)
-        : r(__builtin_amdgcn_make_buffer_rsrc(base, 0, rows * RMPC_WAVE * 16, 0x00020000)),
-          vo((unsigned int)lane * 16u) {}
-    __device__ __forceinline__ double2 ld(int row) const {
-        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-        const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, vo, row * RMPC_WAVE * 16, 0);
-        return __builtin_bit_cast(double2, v);
+    __device__ __forceinline__ WaveRows(void *base, int rows, int lane)
+        : r(__builtin_amdgcn_make_buffer_rsrc(base, 0, rows * RMPC_WAVE * RB, 0x00020000)),
+          vo((unsigned int)lane * RB) {}
+    __device__ __forceinline__ u4v ld16(int row) const {
+        return __builtin_amdgcn_raw_buffer_load_b128(r, vo, row * RMPC_WAVE * RB, 0);
     }
-    __device__ __forceinline__ void st(int row, double2 x) const {
-        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, x), r, vo, row * RMPC_WAVE * 16, 0);
+    __device__ __forceinline__ void st16(int row, u4v x) const {
+        __builtin_amdgcn_raw_buffer_store_b128(x, r, vo, row * RMPC_WAVE * RB, 0);
+    }
+    __device__ __forceinline__ u2v ld8(int row) const {
+        return __builtin_amdgcn_raw_buffer_load_b64(r, vo, row * RMPC_WAVE * RB, 0);
+    }
+    __device__ __forceinline__ void st8(int row, u2v x) const {
+        __builtin_amdgcn_raw_buffer_store_b64(x, r, vo, row * RMPC_WAVE * RB, 0);
     }
 };
 
-template <int N, int BS>
+// The 8 gain values of a block (K rows, k) as 16-byte rows: 4 per block in fp64, 2 in fp32
+template <typename T> struct GainTile;
+template <> struct GainTile<double> {
+    WaveRows<16> w;
+    __device__ __forceinline__ GainTile(void *base, int nb, int lane) : w(base, nb * 4, lane) {}
+    __device__ __forceinline__ void st(int j, const double G[8]) const {
+#pragma unroll
+        for (int q = 0; q < 4; q++) w.st16(j * 4 + q, __builtin_bit_cast(u4v, make_double2(G[2 * q], G[2 * q + 1])));
+    }
+    __device__ __forceinline__ void ld(int j, double G[8]) const {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const double2 v = __builtin_bit_cast(double2, w.ld16(j * 4 + q));
+            G[2 * q] = v.x;
+            G[2 * q + 1] = v.y;
+        }
+    }
+};
+template <> struct GainTile<float> {
+    WaveRows<16> w;
+    __device__ __forceinline__ GainTile(void *base, int nb, int lane) : w(base, nb * 2, lane) {}
+    __device__ __forceinline__ void st(int j, const float G[8]) const {
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+            w.st16(j * 2 + q, __builtin_bit_cast(u4v, make_float4(G[4 * q], G[4 * q + 1], G[4 * q + 2], G[4 * q + 3])));
+    }
+    __device__ __forceinline__ void ld(int j, float G[8]) const {
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const float4 v = __builtin_bit_cast(float4, w.ld16(j * 2 + q));
+            G[4 * q] = v.x; G[4 * q + 1] = v.y; G[4 * q + 2] = v.z; G[4 * q + 3] = v.w;
+        }
+    }
+};
+
+// The block inputs (2 values per block): one 16-byte row in fp64, one 8-byte row in fp32
+template <typename T> struct UsolTile;
+template <> struct UsolTile<double> {
+    WaveRows<16> w;
+    __device__ __forceinline__ UsolTile(void *base, int nb, int lane) : w(base, nb, lane) {}
+    __device__ __forceinline__ void st(int j, double u0, double u1) const {
+        w.st16(j, __builtin_bit_cast(u4v, make_double2(u0, u1)));
+    }
+    __device__ __forceinline__ void ld(int j, double &u0, double &u1) const {
+        const double2 v = __builtin_bit_cast(double2, w.ld16(j));
+        u0 = v.x; u1 = v.y;
+    }
+};
+template <> struct UsolTile<float> {
+    WaveRows<8> w;
+    __device__ __forceinline__ UsolTile(void *base, int nb, int lane) : w(base, nb, lane) {}
+    __device__ __forceinline__ void st(int j, float u0, float u1) const {
+        w.st8(j, __builtin_bit_cast(u2v, make_float2(u0, u1)));
+    }
+    __device__ __forceinline__ void ld(int j, float &u0, float &u1) const {
+        const float2 v = __builtin_bit_cast(float2, w.ld8(j));
+        u0 = v.x; u1 = v.y;
+    }
+};
+
+template <typename T> struct Big;
+template <> struct Big<double> { static constexpr double v = 1e300; };
+template <> struct Big<float> { static constexpr float v = 1e30f; };
+
+template <int N, int BS, typename T>
 __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     constexpr int NB = (N + BS - 1) / BS;
     constexpr int PF = 4;     // gain blocks prefetched ahead in the forward sweep
+    constexpr bool F64 = sizeof(T) == 8;
+    const T BIG = Big<T>::v;
     const int lane = threadIdx.x;
     // Obstacles (x, y, d_safe + r) staged in LDS once: read from global inside the sweeps
     // they compile to vector loads (the pointer may alias the kernel's stores) whose
     // vmcnt(0) waits would drain the gain prefetch at every step.
-    __shared__ double obs_s[3 * RMPC_MAX_OBSTACLES];
+    __shared__ T obs_s[3 * RMPC_MAX_OBSTACLES];
     if (lane < a.no) {
-        obs_s[3 * lane] = a.obs[3 * lane];
-        obs_s[3 * lane + 1] = a.obs[3 * lane + 1];
-        obs_s[3 * lane + 2] = a.prm.d_safe + a.obs[3 * lane + 2];
+        obs_s[3 * lane] = (T)a.obs[3 * lane];
+        obs_s[3 * lane + 1] = (T)a.obs[3 * lane + 1];
+        obs_s[3 * lane + 2] = (T)(a.prm.d_safe + a.obs[3 * lane + 2]);
     }
     __syncthreads();
     const int64_t t = (int64_t)blockIdx.x * RMPC_WAVE + lane;
@@ -62,18 +139,23 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     const int64_t b = a.index ? (int64_t)a.index[t] : t;
     const MpcDevParams &p = a.prm;
     const int no = a.no;
-    const double dt = p.dt, rho = p.rho;
-    const double Q0 = p.Q[0], Q1 = p.Q[1], Q2 = p.Q[2], R0 = p.R[0], R1 = p.R[1];
+    const T dt = (T)p.dt, rho = (T)p.rho;
+    const T Q0 = (T)p.Q[0], Q1 = (T)p.Q[1], Q2 = (T)p.Q[2], R0 = (T)p.R[0], R1 = (T)p.R[1];
+    const T P0 = (T)p.P[0], P1 = (T)p.P[1], P2 = (T)p.P[2];
+    const T vmax = (T)p.v_max, omax = (T)p.omega_max;
     const double *xr = a.x_refs + (size_t)b * a.ref_rows * 3;
     const double *ur = a.u_refs + (size_t)b * a.uref_rows * 2;
-    const WaveRows gt(a.gains + (size_t)blockIdx.x * NB * 4 * RMPC_WAVE, NB * 4, lane);
-    const WaveRows ut(a.usol + (size_t)blockIdx.x * NB * RMPC_WAVE, NB, lane);
+    // per-wave tiles (sized for fp64; fp32 uses half)
+    const GainTile<T> gt(a.gains + (size_t)blockIdx.x * NB * 4 * RMPC_WAVE, NB, lane);
+    const UsolTile<T> ut(a.usol + (size_t)blockIdx.x * NB * RMPC_WAVE, NB, lane);
 
     // ---- setup: np.unwrap'd reference heading, linearisation data (mpc_controller.py:391-428)
     // sin/cos of the heading and the reference speed stay in VGPRs; the reference position
     // and turn rate per step live in LDS ([field][k][lane]: lane-contiguous, conflict-free).
-    extern __shared__ double lds[];
-    double S[N], Cs[N], V0[N];
+    // The unwrap and sin/cos run in fp64 for both T.
+    extern __shared__ double lds_raw[];
+    T *const lds = reinterpret_cast<T *>(lds_raw);
+    T S[N], Cs[N], V0[N];
 #define PX(k) lds[(0 * N + (k)) * RMPC_WAVE + lane]
 #define PY(k) lds[(1 * N + (k)) * RMPC_WAVE + lane]
 #define V1(k) lds[(2 * N + (k)) * RMPC_WAVE + lane]
@@ -86,17 +168,20 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         prev = th;
         const double thu = th + corr;
         if (k == 0) th0 = thu;
-        sincos(thu, &S[k], &Cs[k]);
-        V0[k] = ur[2 * k];
-        V1(k) = ur[2 * k + 1];
-        PX(k) = xr[3 * k];
-        PY(k) = xr[3 * k + 1];
+        double sn, cs;
+        sincos(thu, &sn, &cs);
+        S[k] = (T)sn;
+        Cs[k] = (T)cs;
+        V0[k] = (T)ur[2 * k];
+        V1(k) = (T)ur[2 * k + 1];
+        PX(k) = (T)xr[3 * k];
+        PY(k) = (T)xr[3 * k + 1];
         fin = fin && isfinite(S[k] + Cs[k] + V0[k] + V1(k) + PX(k) + PY(k));
         __builtin_amdgcn_sched_barrier(0);
     }
     const double *x0p = a.x0 + 3 * b;
     const double x0a = th0 + wrap_pi(x0p[2] - th0);                // :397-401
-    const double d0 = x0p[0] - xr[0], d1 = x0p[1] - xr[1], d2 = x0a - th0;
+    const T d0 = (T)(x0p[0] - xr[0]), d1 = (T)(x0p[1] - xr[1]), d2 = (T)(x0a - th0);
     fin = fin && isfinite(d0 + d1 + d2);
 
     uint32_t Hf[N];                   // hinge-row active flags of step k (bit o)
@@ -107,7 +192,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     for (int j = 0; j < NB; j++) Bf[j] = 0;
 
     int it = 0, cert = 0, used = 0;
-    double J = 0.0;
+    T J = 0;
     const int maxit = min(p.max_iter, a.pdas_cap);
     unsigned long long tp_b = 0, tp_f = 0, tp0 = a.prof ? __builtin_amdgcn_s_memtime() : 0ull;
     const unsigned long long tp_setup = tp0;
@@ -123,24 +208,24 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         }
         // ---------------- backward block Riccati sweep
         if (a.prof) tp0 = __builtin_amdgcn_s_memtime();
-        RicV<double> V;
-        V.P00 = p.P[0]; V.P01 = 0; V.P02 = 0; V.P11 = p.P[1]; V.P12 = 0; V.P22 = p.P[2];
-        V.p0 = -p.P[0] * 0.0; V.p1 = -p.P[1] * 0.0; V.p2 = -p.P[2] * 0.0;
+        RicV<T> V;
+        V.P00 = P0; V.P01 = 0; V.P02 = 0; V.P11 = P1; V.P12 = 0; V.P22 = P2;
+        V.p0 = -P0 * (T)0; V.p1 = -P1 * (T)0; V.p2 = -P2 * (T)0;
 #pragma unroll
         for (int j = NB - 1; j >= 0; j--) {
             const int k0 = j * BS;
             const int k1 = (k0 + BS < N) ? k0 + BS : N;
-            RicW<double> W = ric_open(V);
-            double lo0 = -1e300, hi0 = 1e300, lo1 = -1e300, hi1 = 1e300;
+            RicW<T> W = ric_open(V);
+            T lo0 = -BIG, hi0 = BIG, lo1 = -BIG, hi1 = BIG;
 #pragma unroll
             for (int k = k1 - 1; k >= k0; k--) {
-                double q00 = Q0, q01 = 0, q11 = Q1;
-                double qv0 = -Q0 * 0.0, qv1 = -Q1 * 0.0, qv2 = -Q2 * 0.0;
+                T q00 = Q0, q01 = 0, q11 = Q1;
+                T qv0 = -Q0 * (T)0, qv1 = -Q1 * (T)0, qv2 = -Q2 * (T)0;
                 if (k > 0 && Hf[k]) {
                     for (int o = 0; o < no; o++) {      // branch-free: inactive rows add 0
-                        double n0, n1, hb;
+                        T n0, n1, hb;
                         hinge_row_fast(PX(k), PY(k), obs_s[3 * o], obs_s[3 * o + 1], obs_s[3 * o + 2], n0, n1, hb);
-                        const double w = ((Hf[k] >> o) & 1u) ? rho : 0.0;
+                        const T w = ((Hf[k] >> o) & 1u) ? rho : (T)0;
                         q00 += w * n0 * n0;
                         q01 += w * n0 * n1;
                         q11 += w * n1 * n1;
@@ -148,27 +233,24 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                         qv1 -= w * hb * n1;
                     }
                 }
-                const double vr = fabs(V0[k]) > 0.01 ? V0[k] : 0.1;     // :425
-                const double a0 = -vr * S[k] * dt, a1 = vr * Cs[k] * dt;
-                const double b0 = Cs[k] * dt, b1 = S[k] * dt;
+                const T vr = fabs(V0[k]) > (T)0.01 ? V0[k] : (T)0.1;     // :425
+                const T a0 = -vr * S[k] * dt, a1 = vr * Cs[k] * dt;
+                const T b0 = Cs[k] * dt, b1 = S[k] * dt;
                 ric_step(W, a0, a1, b0, b1, dt, q00, q01, q11, Q2, qv0, qv1, qv2, R0, R1,
                          R0 * V0[k], R1 * V1(k));
                 __builtin_amdgcn_sched_barrier(0);   // keep live ranges per step (see header)
             }
 #pragma unroll
             for (int k = k0; k < k1; k++) {                            // :431-436 per block
-                lo0 = fmax(lo0, -p.v_max - V0[k]);
-                hi0 = fmin(hi0, p.v_max - V0[k]);
-                lo1 = fmax(lo1, -p.omega_max - V1(k));
-                hi1 = fmin(hi1, p.omega_max - V1(k));
+                lo0 = fmax(lo0, -vmax - V0[k]);
+                hi0 = fmin(hi0, vmax - V0[k]);
+                lo1 = fmax(lo1, -omax - V1(k));
+                hi1 = fmin(hi1, omax - V1(k));
             }
             const int bf0 = Bf[j] & 3, bf1 = (Bf[j] >> 2) & 3;
-            double G[8];
+            T G[8];
             V = ric_block_bf(W, bf0, bf1, bf0 == 1 ? lo0 : hi0, bf1 == 1 ? lo1 : hi1, G);
-            gt.st(j * 4 + 0, make_double2(G[0], G[1]));
-            gt.st(j * 4 + 1, make_double2(G[2], G[3]));
-            gt.st(j * 4 + 2, make_double2(G[4], G[5]));
-            gt.st(j * 4 + 3, make_double2(G[6], G[7]));
+            gt.st(j, G);
             __builtin_amdgcn_sched_barrier(0);
         }
         if (a.prof) {
@@ -180,56 +262,51 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         // (opaque again: stops CSE from carrying backward-sweep values across this sweep)
 #pragma unroll
         for (int k = 0; k < N; k++) asm volatile("" : "+v"(S[k]), "+v"(Cs[k]), "+v"(V0[k]));
-        const double eps_h = 1e-14, eps_b = 1e-13;
+        const T eps_h = SetTol<T>::hinge, eps_b = SetTol<T>::box;
         int changed = 0;
         used = 0;
-        J = 0.0;
-        double x0 = d0, x1 = d1, x2 = d2;
-        double2 g[NB][4];
+        J = 0;
+        T x0 = d0, x1 = d1, x2 = d2;
+        T g[NB][8];
 #pragma unroll
-        for (int j = 0; j < NB && j < PF; j++)
-#pragma unroll
-            for (int q = 0; q < 4; q++) g[j][q] = gt.ld(j * 4 + q);
+        for (int j = 0; j < NB && j < PF; j++) gt.ld(j, g[j]);
 #pragma unroll
         for (int j = 0; j < NB; j++) {
-            if (j + PF < NB) {
-#pragma unroll
-                for (int q = 0; q < 4; q++) g[j + PF][q] = gt.ld((j + PF) * 4 + q);
-            }
+            if (j + PF < NB) gt.ld(j + PF, g[j + PF]);
             const int k0 = j * BS;
             const int k1 = (k0 + BS < N) ? k0 + BS : N;
-            double lo0 = -1e300, hi0 = 1e300, lo1 = -1e300, hi1 = 1e300;
+            T lo0 = -BIG, hi0 = BIG, lo1 = -BIG, hi1 = BIG;
 #pragma unroll
             for (int k = k0; k < k1; k++) {
-                lo0 = fmax(lo0, -p.v_max - V0[k]);
-                hi0 = fmin(hi0, p.v_max - V0[k]);
-                lo1 = fmax(lo1, -p.omega_max - V1(k));
-                hi1 = fmin(hi1, p.omega_max - V1(k));
+                lo0 = fmax(lo0, -vmax - V0[k]);
+                hi0 = fmin(hi0, vmax - V0[k]);
+                lo1 = fmax(lo1, -omax - V1(k));
+                hi1 = fmin(hi1, omax - V1(k));
             }
-            const double e0 = g[j][0].x * x0 + g[j][0].y * x1 + g[j][1].x * x2 + g[j][3].x;
-            const double e1 = g[j][1].y * x0 + g[j][2].x * x1 + g[j][2].y * x2 + g[j][3].y;
+            const T e0 = g[j][0] * x0 + g[j][1] * x1 + g[j][2] * x2 + g[j][6];
+            const T e1 = g[j][3] * x0 + g[j][4] * x1 + g[j][5] * x2 + g[j][7];
             const int bf0 = Bf[j] & 3, bf1 = (Bf[j] >> 2) & 3;
-            const double u0v = bf0 == 0 ? e0 : (bf0 == 1 ? lo0 : hi0);
-            const double u1v = bf1 == 0 ? e1 : (bf1 == 1 ? lo1 : hi1);
+            const T u0v = bf0 == 0 ? e0 : (bf0 == 1 ? lo0 : hi0);
+            const T u1v = bf1 == 0 ? e1 : (bf1 == 1 ? lo1 : hi1);
             const int ns0 = box_rule(bf0, e0, lo0, hi0, eps_b), ns1 = box_rule(bf1, e1, lo1, hi1, eps_b);
             if (ns0 != bf0 || ns1 != bf1) {
                 changed = 1;
                 Bf[j] = (uint32_t)(ns0 | (ns1 << 2));
             }
-            ut.st(j, make_double2(u0v, u1v));
+            ut.st(j, u0v, u1v);
 #pragma unroll
             for (int k = k0; k < k1; k++) {
                 J += Q0 * x0 * x0 + Q1 * x1 * x1 + Q2 * x2 * x2;
-                const double uu0 = u0v + V0[k], uu1 = u1v + V1(k);
+                const T uu0 = u0v + V0[k], uu1 = u1v + V1(k);
                 J += R0 * uu0 * uu0 + R1 * uu1 * uu1;
                 uint32_t hk = Hf[k];
                 for (int o = 0; o < no; o++) {          // branch-free row update
-                    double n0, n1, hb;
+                    T n0, n1, hb;
                     const bool kept = hinge_row_fast(PX(k), PY(k), obs_s[3 * o], obs_s[3 * o + 1], obs_s[3 * o + 2], n0, n1, hb);
-                    const double r = kept ? hb - n0 * x0 - n1 * x1 : -1.0;   // unkept: never active
-                    const double rp = fmax(r, 0.0);
+                    const T r = kept ? hb - n0 * x0 - n1 * x1 : (T)-1;   // unkept: never active
+                    const T rp = fmax(r, (T)0);
                     J += rho * rp * rp;
-                    used |= (r > 1e-6);                                        // :485
+                    used |= (r > (T)1e-6);                                     // :485
                     if (k > 0) {
                         const uint32_t act = (hk >> o) & 1u;
                         const uint32_t na = act ? (r > -eps_h) : (r > eps_h);
@@ -238,19 +315,19 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                     }
                 }
                 Hf[k] = hk;
-                const double vr = fabs(V0[k]) > 0.01 ? V0[k] : 0.1;
-                const double n0 = x0 + (-vr * S[k] * dt) * x2 + (Cs[k] * dt) * u0v;
-                const double n1 = x1 + (vr * Cs[k] * dt) * x2 + (S[k] * dt) * u0v;
-                const double n2 = x2 + dt * u1v;
+                const T vr = fabs(V0[k]) > (T)0.01 ? V0[k] : (T)0.1;
+                const T n0 = x0 + (-vr * S[k] * dt) * x2 + (Cs[k] * dt) * u0v;
+                const T n1 = x1 + (vr * Cs[k] * dt) * x2 + (S[k] * dt) * u0v;
+                const T n2 = x2 + dt * u1v;
                 x0 = n0; x1 = n1; x2 = n2;
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        J += p.P[0] * x0 * x0 + p.P[1] * x1 * x1 + p.P[2] * x2 * x2;
+        J += P0 * x0 * x0 + P1 * x1 * x1 + P2 * x2 * x2;
         if (a.prof) tp_f += __builtin_amdgcn_s_memtime() - tp0;
         if (!changed) { cert = 1; break; }
         // PDAS cycling: a repeated active-set signature hands the robot to the
-        // projected-Newton phase of the generic kernel
+        // projected-Newton phase of the next stage
         uint64_t sig = 1469598103934665603ull;
 #pragma unroll
         for (int k = 0; k < N; k++) sig = (sig ^ (uint64_t)Hf[k]) * 1099511628211ull;
@@ -290,18 +367,21 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
 #pragma unroll
     for (int k = 0; k < N; k++) asm volatile("" : "+v"(S[k]), "+v"(Cs[k]), "+v"(V0[k]));
     // ---- outputs (mpc_controller.py:484-520): x_pred = x_refs + dx (not unwrapped),
-    // u = u_refs + du, omega ramp, step counter
+    // u = u_refs + du, omega ramp, step counter.  In fp32 the fp64 references are re-read so
+    // that only the deviations carry fp32 rounding.
     const int sc = a.step_count ? a.step_count[b] : 0;
-    double x0 = d0, x1 = d1, x2 = d2;
+    T x0 = d0, x1 = d1, x2 = d2;
     double uc0 = 0, uc1 = 0;
 #pragma unroll
     for (int j = 0; j < NB; j++) {
-        const double2 u = ut.ld(j);
+        T du0, du1;
+        ut.ld(j, du0, du1);
         const int k0 = j * BS;
         const int k1 = (k0 + BS < N) ? k0 + BS : N;
 #pragma unroll
         for (int k = k0; k < k1; k++) {
-            double v0 = u.x + V0[k], v1 = u.y + V1(k);
+            double v0 = F64 ? (double)(du0 + V0[k]) : (double)du0 + ur[2 * k];
+            double v1 = F64 ? (double)(du1 + V1(k)) : (double)du1 + ur[2 * k + 1];
             if (k == 0) {
                 if (sc < p.ramp_up_steps) {                           // :502-505
                     const double lim = p.omega_max * ((double)(sc + 1) / (double)p.ramp_up_steps);
@@ -316,27 +396,27 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             }
             if (a.x_pred) {
                 double *xp = a.x_pred + ((size_t)b * (N + 1) + k) * 3;
-                xp[0] = x0 + PX(k);
-                xp[1] = x1 + PY(k);
-                xp[2] = x2 + xr[3 * k + 2];
+                xp[0] = F64 ? (double)(x0 + PX(k)) : (double)x0 + xr[3 * k];
+                xp[1] = F64 ? (double)(x1 + PY(k)) : (double)x1 + xr[3 * k + 1];
+                xp[2] = (double)x2 + xr[3 * k + 2];
             }
-            const double vr = fabs(V0[k]) > 0.01 ? V0[k] : 0.1;
-            const double n0 = x0 + (-vr * S[k] * dt) * x2 + (Cs[k] * dt) * u.x;
-            const double n1 = x1 + (vr * Cs[k] * dt) * x2 + (S[k] * dt) * u.x;
-            const double n2 = x2 + dt * u.y;
+            const T vr = fabs(V0[k]) > (T)0.01 ? V0[k] : (T)0.1;
+            const T n0 = x0 + (-vr * S[k] * dt) * x2 + (Cs[k] * dt) * du0;
+            const T n1 = x1 + (vr * Cs[k] * dt) * x2 + (S[k] * dt) * du0;
+            const T n2 = x2 + dt * du1;
             x0 = n0; x1 = n1; x2 = n2;
         }
     }
     if (a.x_pred) {
         double *xp = a.x_pred + ((size_t)b * (N + 1) + N) * 3;
-        xp[0] = x0 + xr[3 * N];
-        xp[1] = x1 + xr[3 * N + 1];
-        xp[2] = x2 + xr[3 * N + 2];
+        xp[0] = (double)x0 + xr[3 * N];
+        xp[1] = (double)x1 + xr[3 * N + 1];
+        xp[2] = (double)x2 + xr[3 * N + 2];
     }
     if (a.step_count) a.step_count[b] = sc + 1;                        // :507
     a.u0[2 * b] = uc0;
     a.u0[2 * b + 1] = uc1;
-    if (a.cost) a.cost[b] = J;
+    if (a.cost) a.cost[b] = (double)J;
     if (a.slack_used) a.slack_used[b] = (uint8_t)used;
     a.status[b] = RMPC_OPTIMAL;
     if (a.iters) a.iters[b] = it;
@@ -350,19 +430,26 @@ using namespace rmpc;
 #undef PY
 #undef V1
 
-bool rmpc_mpc_fast_supported(int N, int bs) {
+bool rmpc_mpc_fast_supported(int N, int bs, int prec) {
+    if (prec == RMPC_F32) return bs == 1 && (N == 20 || N == 30);
     return (bs == 1 && (N == 6 || N == 10 || N == 20)) || (bs == 2 && N == 6);
 }
 
-hipError_t rmpc_launch_mpc_fast_f64(const MpcFastArgs &a, int N, int bs, hipStream_t stream) {
+hipError_t rmpc_launch_mpc_fast(const MpcFastArgs &a, int N, int bs, int prec, hipStream_t stream) {
     const int64_t n = a.B;
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + RMPC_WAVE - 1) / RMPC_WAVE)), block(RMPC_WAVE);
-    const size_t lds = (size_t)3 * N * RMPC_WAVE * sizeof(double);
-    if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1>), grid, block, lds, stream, a);
-    else if (bs == 1 && N == 10) hipLaunchKernelGGL((mpc_ltv_fast_kernel<10, 1>), grid, block, lds, stream, a);
-    else if (bs == 1 && N == 6) hipLaunchKernelGGL((mpc_ltv_fast_kernel<6, 1>), grid, block, lds, stream, a);
-    else if (bs == 2 && N == 6) hipLaunchKernelGGL((mpc_ltv_fast_kernel<6, 2>), grid, block, lds, stream, a);
-    else return hipErrorInvalidValue;
+    const size_t lds = (size_t)3 * N * RMPC_WAVE * (prec == RMPC_F32 ? sizeof(float) : sizeof(double));
+    if (prec == RMPC_F32) {
+        if (bs == 1 && N == 30) hipLaunchKernelGGL((mpc_ltv_fast_kernel<30, 1, float>), grid, block, lds, stream, a);
+        else if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, float>), grid, block, lds, stream, a);
+        else return hipErrorInvalidValue;
+    } else {
+        if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double>), grid, block, lds, stream, a);
+        else if (bs == 1 && N == 10) hipLaunchKernelGGL((mpc_ltv_fast_kernel<10, 1, double>), grid, block, lds, stream, a);
+        else if (bs == 1 && N == 6) hipLaunchKernelGGL((mpc_ltv_fast_kernel<6, 1, double>), grid, block, lds, stream, a);
+        else if (bs == 2 && N == 6) hipLaunchKernelGGL((mpc_ltv_fast_kernel<6, 2, double>), grid, block, lds, stream, a);
+        else return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }

@@ -138,6 +138,19 @@ __device__ __forceinline__ RicV<T> ric_block(const RicW<T> &s, int bf0, int bf1,
     return v;
 }
 
+__device__ __forceinline__ double fast_rcp(double x) { return __builtin_amdgcn_rcp(x); }
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// Active-set tolerances per arithmetic: fp64 certifies to ~1e-14; fp32 to its own rounding
+// level, else rows sitting on their boundary flip on rounding noise.
+template <typename T> struct SetTol;
+template <> struct SetTol<double> {
+    static constexpr double hinge = 1e-14, box = 1e-13, pn = 1e-6;
+};
+template <> struct SetTol<float> {
+    static constexpr float hinge = 2e-6f, box = 1e-5f, pn = 1e-4f;
+};
+
 // Branch-free variant of ric_block for the register-resident kernel: the four free/fixed
 // cases as ONE masked 2x2 solve (a fixed component's row/column of Wuu becomes the
 // identity and its right-hand side the bound), and the determinant's reciprocal from
@@ -151,7 +164,7 @@ __device__ __forceinline__ RicV<T> ric_block_bf(const RicW<T> &s, int bf0, int b
     const T m00 = fr0 ? s.U00 : (T)1, m11 = fr1 ? s.U11 : (T)1;
     const T m01 = (fr0 && fr1) ? s.U01 : (T)0;
     const T det = m00 * m11 - m01 * m01;
-    T id = __builtin_amdgcn_rcp(det);
+    T id = fast_rcp(det);
     id = id * ((T)2 - det * id);
     id = id * ((T)2 - det * id);
     const T i00 = m11 * id, i01 = -m01 * id, i11 = m00 * id;
@@ -233,6 +246,19 @@ __device__ __forceinline__ bool hinge_row_fast(double px, double py, double ox, 
     n0 = ddx * y;
     n1 = ddy * y;
     hb = safe - (n0 * (px - ox) + n1 * (py - oy));
+    return kept;
+}
+
+// fp32 overload (v_rsq_f32 is accurate to ~1 ulp of float: no Newton step needed)
+__device__ __forceinline__ bool hinge_row_fast(float px, float py, float ox, float oy, float safe,
+                                                 float &n0, float &n1, float &hb) {
+    const float ddx = px - ox, ddy = py - oy;
+    const float d2 = ddx * ddx + ddy * ddy;
+    const float y = __builtin_amdgcn_rsqf(d2);
+    const bool kept = d2 * y > 0.01f;
+    n0 = ddx * y;
+    n1 = ddy * y;
+    hb = safe - (n0 * ddx + n1 * ddy);
     return kept;
 }
 

@@ -1,0 +1,10 @@
+#!/bin/bash
+# cfg4 (fp32, N=30, 8 obstacles): iteration histogram, then a fast-cap sweep of the bench
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+RMPC_FAST_CAP=64 RMPC_DISABLE_DENSE=1 timeout -k 10 300 python scripts/iter_hist.py cfg4 > gpurun_out/ih4.txt 2>&1 || exit $?
+grep -v amdgpu.ids gpurun_out/ih4.txt
+for v in "$@"; do
+  [ "$v" = "-" ] && v=""
+  env $v timeout -k 10 300 python bench.py --config cfg4 --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/c4.json 2>gpurun_out/c4.err || exit $?
+  python -c "import json;d=json.load(open('gpurun_out/c4.json'));r=d['roofline'];print('[$v] value %.3e ms %.3f'%(d['value'],d['ms_per_step']), {k:round(v,3) for k,v in r['stage_ms'].items()})"
+done

@@ -415,14 +415,22 @@ def test_simulation_drop_ins_match_logs_and_oracle(rm, golden, tmp_path):
 
 
 @pytest.mark.gpu
-def test_mpc_fp32_config4_accuracy(rm, capsys):
-    """BASELINE config 4 arithmetic (fp32, N=30, 8 obstacles) against the fp64 C port on the
+@pytest.mark.parametrize("N,obs_kind", [(30, "union8"), (20, "default")])
+@pytest.mark.parametrize("stage", ["pipeline", "dense_only", "generic_only"])
+def test_mpc_fp32_config4_accuracy(rm, capsys, monkeypatch, N, obs_kind, stage):
+    """BASELINE config 4 arithmetic (fp32; N=30, 8 obstacles) against the fp64 C port on the
     same inputs: the achieved control error is measured and reported ("report
-    achieved relative error honestly")."""
-    B, N = 2048, 30
+    achieved relative error honestly").  Each stage of the fp32 pipeline is also run alone:
+    the lane-per-robot fp32 kernel with its fp64 dense tail (pipeline), every robot through
+    the dense tail (RMPC_FAST_CAP=0), and the fp32 generic kernel (RMPC_DISABLE_FAST)."""
+    if stage == "dense_only":
+        monkeypatch.setenv("RMPC_FAST_CAP", "0")
+    elif stage == "generic_only":
+        monkeypatch.setenv("RMPC_DISABLE_FAST", "1")
+    B = 2048
     t0 = (np.arange(B) / B) * (2 * np.pi / 0.5)
     x0, xr, ur = _workload(N, B, 2, t0=t0)
-    obs = ompc.union8_obstacles()
+    obs = ompc.union8_obstacles() if obs_kind == "union8" else ompc.default_obstacles()
     p = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02,
                               precision=1)
     out = rm.batch.mpc_solve_batch(p, x0, xr, ur, obs)
@@ -432,6 +440,6 @@ def test_mpc_fp32_config4_accuracy(rm, capsys):
     assert both.mean() >= 0.99
     rel = np.abs(out["u0"] - ref["u0"]).max(axis=1) / np.maximum(1.0, np.abs(ref["u0"]).max(axis=1))
     with capsys.disabled():
-        print(f"\n[fp32 cfg4] status ok {both.mean():.4f}; rel |du0|: median {np.median(rel[both]):.2e} "
-              f"p99 {np.percentile(rel[both], 99):.2e} max {rel[both].max():.2e}")
+        print(f"\n[fp32 N={N} {stage}] status ok {both.mean():.4f}; rel |du0|: median "
+              f"{np.median(rel[both]):.2e} p99 {np.percentile(rel[both], 99):.2e} max {rel[both].max():.2e}")
     assert rel[both].max() <= 1e-4          # the north star's control-error bound
