@@ -332,14 +332,46 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         dbg_sync(s, "fast");
         const int32_t *left = (const int32_t *)c->retry.p;
         const int32_t *left_n = (const int32_t *)c->retry_count.p;
-        if (rmpc_mpc_dense_supported(p->horizon, bs, n_obs) && !getenv("RMPC_DISABLE_DENSE")) {
+        // tail: the lane-group Riccati kernel (default) or the condensed wave-per-robot one
+        // (RMPC_TAIL=dense); RMPC_DISABLE_DENSE skips the tail stage altogether
+        const char *tail = getenv("RMPC_TAIL");
+        const bool use_dense = tail && !strcmp(tail, "dense");
+        const int tail_cap = getenv("RMPC_DENSE_CAP") ? atoi(getenv("RMPC_DENSE_CAP")) : 4;
+        if (!use_dense && rmpc_mpc_group_supported(p->horizon, bs, n_obs) && !getenv("RMPC_DISABLE_DENSE")) {
+            HIP_TRY(c->retry2.ensure((size_t)B * sizeof(int32_t)));
+            int32_t *cnt2 = (int32_t *)c->retry_count.p + 8;
+            HIP_TRY(rmpc_launch_mpc_group(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs, uref_rows,
+                                          obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
+                                          iters, left, left_n, (int32_t *)c->retry2.p, cnt2, tail_cap,
+                                          a.retry_sets, s, pc));
+            if (prof) {
+                unsigned long long h[64];
+                int32_t cn[16];
+                HIP_TRY(hipMemcpyAsync(h, pc, sizeof(h), hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipMemcpyAsync(cn, c->retry_count.p, sizeof(cn), hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipStreamSynchronize(s));
+                const double r = h[10] ? (double)h[10] : 1.0, li = h[9] ? (double)h[9] : 1.0;
+                fprintf(stderr,
+                        "[group] in=%d out=%d rounds=%llu loop-its/round %.2f | cycles/round: setup %.0f pn-pre %.0f "
+                        "out %.0f upd %.0f ls %.0f | per loop-it: weights %.0f back %.0f fwd %.0f rows %.0f\n",
+                        cn[0], cn[8], h[10], h[9] / r, h[0] / r, h[1] / r, h[6] / r, h[7] / r, h[8] / r,
+                        h[2] / li, h[3] / li, h[4] / li, h[5] / li);
+                const double w = h[20] ? (double)h[20] : 1.0;
+                fprintf(stderr, "[fast] waves=%llu per wave: total %.0f back %.0f fwd %.0f iters %.2f | per iter: back %.0f fwd %.0f\n",
+                        h[20], h[19] / w, h[16] / w, h[17] / w, h[18] / w, h[16] / (double)(h[18] ? h[18] : 1),
+                        h[17] / (double)(h[18] ? h[18] : 1));
+            }
+            dbg_sync(s, "group");
+            left = (const int32_t *)c->retry2.p;
+            left_n = cnt2;
+        } else if (rmpc_mpc_dense_supported(p->horizon, bs, n_obs) && !getenv("RMPC_DISABLE_DENSE")) {
             HIP_TRY(c->retry2.ensure((size_t)B * sizeof(int32_t)));
             int32_t *cnt2 = (int32_t *)c->retry_count.p + 8;
             HIP_TRY(rmpc_launch_mpc_dense_f64(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs,
                                               uref_rows, obstacles, step_count, u0, u_seq, x_pred, cost,
                                               status, slack_used, iters, left, left_n,
                                               (int32_t *)c->retry2.p, cnt2, (int32_t *)c->retry_count.p + 12,
-                                              getenv("RMPC_DENSE_CAP") ? atoi(getenv("RMPC_DENSE_CAP")) : 4,
+                                              tail_cap,
                                               a.retry_sets, s, pc));
             if (prof) {
                 unsigned long long h[64];

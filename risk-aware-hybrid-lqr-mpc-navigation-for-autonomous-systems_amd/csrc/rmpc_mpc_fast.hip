@@ -215,10 +215,10 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         for (int j = NB - 1; j >= 0; j--) {
             const int k0 = j * BS;
             const int k1 = (k0 + BS < N) ? k0 + BS : N;
-            RicW<T> W = ric_open(V);
-            T lo0 = -BIG, hi0 = BIG, lo1 = -BIG, hi1 = BIG;
-#pragma unroll
-            for (int k = k1 - 1; k >= k0; k--) {
+            T G[8];
+            if constexpr (BS == 1) {
+                // single-step block: the fused step (rmpc_riccati.h ric_step1_bf)
+                const int k = j;
                 T q00 = Q0, q01 = 0, q11 = Q1;
                 T qv0 = -Q0 * (T)0, qv1 = -Q1 * (T)0, qv2 = -Q2 * (T)0;
                 if (k > 0 && Hf[k]) {
@@ -236,20 +236,47 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                 const T vr = fabs(V0[k]) > (T)0.01 ? V0[k] : (T)0.1;     // :425
                 const T a0 = -vr * S[k] * dt, a1 = vr * Cs[k] * dt;
                 const T b0 = Cs[k] * dt, b1 = S[k] * dt;
-                ric_step(W, a0, a1, b0, b1, dt, q00, q01, q11, Q2, qv0, qv1, qv2, R0, R1,
-                         R0 * V0[k], R1 * V1(k));
-                __builtin_amdgcn_sched_barrier(0);   // keep live ranges per step (see header)
-            }
+                const T lo0 = -vmax - V0[k], hi0 = vmax - V0[k];       // :431-436
+                const T lo1 = -omax - V1(k), hi1 = omax - V1(k);
+                const int bf0 = Bf[j] & 3, bf1 = (Bf[j] >> 2) & 3;
+                V = ric_step1_bf(V, a0, a1, b0, b1, dt, q00, q01, q11, Q2, qv0, qv1, qv2, R0, R1,
+                                 R0 * V0[k], R1 * V1(k), bf0, bf1, bf0 == 1 ? lo0 : hi0, bf1 == 1 ? lo1 : hi1, G);
+            } else {
+                RicW<T> W = ric_open(V);
+                T lo0 = -BIG, hi0 = BIG, lo1 = -BIG, hi1 = BIG;
 #pragma unroll
-            for (int k = k0; k < k1; k++) {                            // :431-436 per block
-                lo0 = fmax(lo0, -vmax - V0[k]);
-                hi0 = fmin(hi0, vmax - V0[k]);
-                lo1 = fmax(lo1, -omax - V1(k));
-                hi1 = fmin(hi1, omax - V1(k));
+                for (int k = k1 - 1; k >= k0; k--) {
+                    T q00 = Q0, q01 = 0, q11 = Q1;
+                    T qv0 = -Q0 * (T)0, qv1 = -Q1 * (T)0, qv2 = -Q2 * (T)0;
+                    if (k > 0 && Hf[k]) {
+                        for (int o = 0; o < no; o++) {      // branch-free: inactive rows add 0
+                            T n0, n1, hb;
+                            hinge_row_fast(PX(k), PY(k), obs_s[3 * o], obs_s[3 * o + 1], obs_s[3 * o + 2], n0, n1, hb);
+                            const T w = ((Hf[k] >> o) & 1u) ? rho : (T)0;
+                            q00 += w * n0 * n0;
+                            q01 += w * n0 * n1;
+                            q11 += w * n1 * n1;
+                            qv0 -= w * hb * n0;
+                            qv1 -= w * hb * n1;
+                        }
+                    }
+                    const T vr = fabs(V0[k]) > (T)0.01 ? V0[k] : (T)0.1;     // :425
+                    const T a0 = -vr * S[k] * dt, a1 = vr * Cs[k] * dt;
+                    const T b0 = Cs[k] * dt, b1 = S[k] * dt;
+                    ric_step(W, a0, a1, b0, b1, dt, q00, q01, q11, Q2, qv0, qv1, qv2, R0, R1,
+                             R0 * V0[k], R1 * V1(k));
+                    __builtin_amdgcn_sched_barrier(0);   // keep live ranges per step (see header)
+                }
+#pragma unroll
+                for (int k = k0; k < k1; k++) {                            // :431-436 per block
+                    lo0 = fmax(lo0, -vmax - V0[k]);
+                    hi0 = fmin(hi0, vmax - V0[k]);
+                    lo1 = fmax(lo1, -omax - V1(k));
+                    hi1 = fmin(hi1, omax - V1(k));
+                }
+                const int bf0 = Bf[j] & 3, bf1 = (Bf[j] >> 2) & 3;
+                V = ric_block_bf(W, bf0, bf1, bf0 == 1 ? lo0 : hi0, bf1 == 1 ? lo1 : hi1, G);
             }
-            const int bf0 = Bf[j] & 3, bf1 = (Bf[j] >> 2) & 3;
-            T G[8];
-            V = ric_block_bf(W, bf0, bf1, bf0 == 1 ? lo0 : hi0, bf1 == 1 ? lo1 : hi1, G);
             gt.st(j, G);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -276,23 +303,26 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             const int k0 = j * BS;
             const int k1 = (k0 + BS < N) ? k0 + BS : N;
             T lo0 = -BIG, hi0 = BIG, lo1 = -BIG, hi1 = BIG;
+            if constexpr (BS == 1) {
+                lo0 = -vmax - V0[k0]; hi0 = vmax - V0[k0];
+                lo1 = -omax - V1(k0); hi1 = omax - V1(k0);
+            } else {
 #pragma unroll
-            for (int k = k0; k < k1; k++) {
-                lo0 = fmax(lo0, -vmax - V0[k]);
-                hi0 = fmin(hi0, vmax - V0[k]);
-                lo1 = fmax(lo1, -omax - V1(k));
-                hi1 = fmin(hi1, omax - V1(k));
+                for (int k = k0; k < k1; k++) {
+                    lo0 = fmax(lo0, -vmax - V0[k]);
+                    hi0 = fmin(hi0, vmax - V0[k]);
+                    lo1 = fmax(lo1, -omax - V1(k));
+                    hi1 = fmin(hi1, omax - V1(k));
+                }
             }
             const T e0 = g[j][0] * x0 + g[j][1] * x1 + g[j][2] * x2 + g[j][6];
             const T e1 = g[j][3] * x0 + g[j][4] * x1 + g[j][5] * x2 + g[j][7];
             const int bf0 = Bf[j] & 3, bf1 = (Bf[j] >> 2) & 3;
             const T u0v = bf0 == 0 ? e0 : (bf0 == 1 ? lo0 : hi0);
             const T u1v = bf1 == 0 ? e1 : (bf1 == 1 ? lo1 : hi1);
-            const int ns0 = box_rule(bf0, e0, lo0, hi0, eps_b), ns1 = box_rule(bf1, e1, lo1, hi1, eps_b);
-            if (ns0 != bf0 || ns1 != bf1) {
-                changed = 1;
-                Bf[j] = (uint32_t)(ns0 | (ns1 << 2));
-            }
+            const int ns0 = box_rule_bf(bf0, e0, lo0, hi0, eps_b), ns1 = box_rule_bf(bf1, e1, lo1, hi1, eps_b);
+            changed |= (int)(ns0 != bf0 || ns1 != bf1);
+            Bf[j] = (uint32_t)(ns0 | (ns1 << 2));
             ut.st(j, u0v, u1v);
 #pragma unroll
             for (int k = k0; k < k1; k++) {

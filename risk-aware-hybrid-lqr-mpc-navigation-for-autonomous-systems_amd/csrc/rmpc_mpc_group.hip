@@ -1,0 +1,694 @@
+// rmpc_mpc_group.hip -- lane-group-per-robot MPC tail solver (Riccati form).
+//
+// The lane-per-robot kernel (rmpc_mpc_fast.hip) runs one robot per lane: every quantity of
+// an active-set iteration -- the hinge rows of every step and obstacle, the box bounds, the
+// set rules, the objective terms -- sits on that lane's sequential instruction stream next
+// to the Riccati recursion, ~15k instructions per iteration.  For the few robots that need
+// many iterations this stream is the launch's critical path.
+//
+// Here a group of G lanes (G = 16: four robots per wave) owns one robot.  Only the two
+// recursions stay sequential -- the backward block Riccati sweep (rmpc_riccati.h, the same
+// algebra as the other kernels) and the forward state/input sweep, both computed
+// redundantly by the group's lanes from LDS broadcasts.  Everything else is spread over the
+// group: the linearisation and hinge rows are built once per robot (step k on lane k mod G),
+// each iteration's per-step hinge weights, set tests, cost terms, hinge forces and box
+// rules run lane-parallel over steps or blocks, and group reductions go through shuffles.
+//
+// Algorithm (identical to the condensed tail in rmpc_mpc_dense.hip, which it replaces):
+// PDAS from the previous stage's active sets (cap + cycle detection), then projected Newton
+// with an Armijo search along the projection arc, every candidate certified by the
+// set-reproduction test, so the result is the QP's exact optimum.  Robots that do not
+// certify (or carry non-finite data) go on to the generic kernel.
+//
+// The groups of a wave run in lockstep (one shared loop; a group that is done is masked),
+// LTV formulation (mpc_controller.py:345-522).
+#include "rmpc_device.h"
+#include "rmpc_internal.h"
+#include "rmpc_riccati.h"
+
+#include <cstdlib>
+
+namespace rmpc {
+
+struct GroupArgs {
+    MpcDevParams prm;
+    int no;
+    const double *x0, *x_refs, *u_refs, *obs;
+    int ref_rows, uref_rows;
+    int32_t *step_count;
+    double *u0, *u_seq, *x_pred, *cost;
+    int32_t *status, *iters;
+    uint8_t *slack_used;
+    const int32_t *index, *count;     // robots to solve (device-side length)
+    int32_t *retry, *retry_count;     // not certified / non-finite -> generic kernel
+    const uint32_t *warm;             // per list entry: hinge flags [N], box states [NB], iters
+    int pdas_cap;                     // PDAS solves before projected Newton
+    unsigned long long *prof;         // optional per-phase cycle counters (diagnostics)
+};
+
+// diagnostics: s_memtime deltas per phase (wave-uniform), flushed once per robot round
+#define GPROF(slot)                                                                   \
+    do {                                                                              \
+        if (prof_on) {                                                                \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();               \
+            pacc[slot] += t_ - tprof;                                                 \
+            tprof = t_;                                                               \
+        }                                                                             \
+    } while (0)
+
+// One robot's LDS record (doubles).  Every region but the hinge rows has a compile-time
+// offset, so the optimiser can prove the recursions' stores (gains, trajectory) disjoint
+// from their loads (step data) and issue the loads ahead; per-step and per-block data are
+// packed 16-byte aligned records (ds_read_b128).
+template <int N, int NB>
+struct GRec {
+    static constexpr int STEP = 0;                 // [N][12]: a0 a1 b0 b1 us0 us1 q00 q01 q11 qv0 qv1 -
+    static constexpr int BLK = STEP + 12 * N;      // [NB][12]: lo0 hi0 lo1 hi1 G0..G7
+    static constexpr int XS = BLK + 12 * NB;       // [N+1][4]: trajectory deviations (x, y, th, -)
+    static constexpr int ZC = XS + 4 * (N + 1);    // candidate of the last solve [2NB]
+    static constexpr int ZZ = ZC + 2 * NB;         // projected-Newton iterate
+    static constexpr int ZT = ZZ + 2 * NB;         // line-search trial point
+    static constexpr int GR = ZT + 2 * NB;         // gradient at ZZ
+    static constexpr int FR = GR + 2 * NB;         // hinge forces per step [N][2]
+    static constexpr int INT = FR + 2 * N;         // uint32: HF [N], BF [NB], NHF [N], NBF [NB]
+    static constexpr int HR = INT + (N + NB + 1) / 2 * 2;   // hinge rows [3][no][N] (runtime no)
+    __host__ __device__ static int size(int no) {
+        const int o = HR + 3 * no * N;
+        return o + (8 - o % 32 + 32) % 32;         // stride = 8 (mod 32) doubles: the groups'
+    }                                              // broadcast reads fall on different banks
+};
+
+template <int G>
+__device__ __forceinline__ bool gany(bool v, int grp) {
+    const uint64_t m = __ballot(v);
+    if (G == 64) return m != 0;
+    return ((m >> (grp * G)) & ((1ull << G) - 1)) != 0;
+}
+
+template <int G>
+__device__ __forceinline__ double gsum(double v) {
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+template <int G>
+__device__ __forceinline__ double gmaxv(double v) {
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+    return v;
+}
+
+enum { PH_PDAS = 0, PH_PN = 1, PH_DONE = 2, PH_IDLE = 3 };
+
+// Stores from inside the uniform recursions: the group's first lane writes the record, the
+// others a private junk slot -- a select of two provably disjoint addresses instead of a
+// branch, so the sweep stays one basic block and the scheduler can issue the next steps'
+// LDS loads ahead of these stores.
+__shared__ double grp_junk[64];
+
+template <int N, int BS, int G>
+__device__ __forceinline__ void group_solve(const GroupArgs &a, double *const base0,
+                                            int t, bool have, int gl, int grp) {
+    constexpr int NB = (N + BS - 1) / BS;
+    constexpr int KPL = (N + G - 1) / G;          // steps per lane
+    const MpcDevParams &p = a.prm;
+    const int no = a.no;
+    const double dt = p.dt, rho = p.rho;
+    const double Q0 = p.Q[0], Q1 = p.Q[1], Q2 = p.Q[2], R0 = p.R[0], R1 = p.R[1];
+    const double P0 = p.P[0], P1 = p.P[1], P2 = p.P[2];
+    const double eps_h = SetTol<double>::hinge, eps_b = SetTol<double>::box;
+    const int64_t b = have ? (int64_t)a.index[t] : 0;
+    const double *xr = a.x_refs + (size_t)b * a.ref_rows * 3;
+    const double *ur = a.u_refs + (size_t)b * a.uref_rows * 2;
+    const bool prof_on = a.prof != nullptr;
+    unsigned long long tprof = prof_on ? __builtin_amdgcn_s_memtime() : 0ull;
+    unsigned long long pacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+
+    // LDS views, re-derived from an opaque offset before each use so that the optimiser
+    // cannot hoist the (loop-invariant) per-step data out of the iteration loop
+    double *base = base0;
+    double *const junk = grp_junk + threadIdx.x;
+#define GST(ref, v) (*(gl == 0 ? &(ref) : junk) = (v))
+#define GSTM(ref, v, m) (*((m) && gl == 0 ? &(ref) : junk) = (v))
+    auto refresh = [&]() __attribute__((always_inline)) {
+        int o = 0;
+        asm volatile("" : "+v"(o));
+        base = base0 + o;
+    };
+    using RC = GRec<N, NB>;
+#define STG(f, k) base[RC::STEP + 12 * (k) + (f)]
+#define WQ(k, f) base[RC::STEP + 12 * (k) + 6 + (f)]
+#define BND(f, j) base[RC::BLK + 12 * (j) + (f)]
+#define GN(j, f) base[RC::BLK + 12 * (j) + 4 + (f)]
+#define HN0(o, k) base[RC::HR + (o) * N + (k)]
+#define HN1(o, k) base[RC::HR + (no + (o)) * N + (k)]
+#define HB(o, k) base[RC::HR + (2 * no + (o)) * N + (k)]
+#define XS(k, d) base[RC::XS + 4 * (k) + (d)]
+#define ZC(i) base[RC::ZC + (i)]
+#define ZZ(i) base[RC::ZZ + (i)]
+#define ZT(i) base[RC::ZT + (i)]
+#define GR(i) base[RC::GR + (i)]
+#define FR(c, k) base[RC::FR + 2 * (k) + (c)]
+#define HF(k) reinterpret_cast<uint32_t *>(base + RC::INT)[(k)]
+#define BF(j) reinterpret_cast<uint32_t *>(base + RC::INT)[N + (j)]
+#define NHF(k) reinterpret_cast<uint32_t *>(base + RC::INT)[N + NB + (k)]
+#define NBF(j) reinterpret_cast<uint32_t *>(base + RC::INT)[2 * N + NB + (j)]
+
+    // ---- setup (mpc_controller.py:391-468): unwrap (sequential, every lane), then the
+    // linearisation and the hinge rows of this lane's steps, the blocked box per block
+    double thl[KPL];
+    double corr = 0.0, prev = xr[2], th0 = 0.0;
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        const double th = xr[3 * k + 2];
+        if (k > 0) corr += unwrap_step(prev, th);
+        prev = th;
+        const double thu = th + corr;
+        if (k == 0) th0 = thu;
+        if (k % G == gl) thl[k / G] = thu;
+    }
+    bool fin = true;
+#pragma unroll
+    for (int i = 0; i < KPL; i++) {
+        const int k = gl + G * i;
+        if (k < N) {
+            double sn, cs;
+            sincos(thl[i], &sn, &cs);
+            const double v = ur[2 * k], w = ur[2 * k + 1];
+            const double vr = fabs(v) > 0.01 ? v : 0.1;                    // :425
+            STG(0, k) = -vr * sn * dt;
+            STG(1, k) = vr * cs * dt;
+            STG(2, k) = cs * dt;
+            STG(3, k) = sn * dt;
+            STG(4, k) = v;
+            STG(5, k) = w;
+            const double px = xr[3 * k], py = xr[3 * k + 1];
+            fin = fin && isfinite(sn + cs + v + w + px + py);
+            for (int o = 0; o < no; o++) {
+                double n0, n1, hb;
+                if (!hinge_row_fast(px, py, a.obs[3 * o], a.obs[3 * o + 1], p.d_safe + a.obs[3 * o + 2], n0, n1, hb)) {
+                    n0 = 0; n1 = 0; hb = -1e300;                             // row not kept
+                }
+                HN0(o, k) = n0;
+                HN1(o, k) = n1;
+                HB(o, k) = hb;
+            }
+        }
+    }
+    for (int j = gl; j < NB; j += G) {                                      // :431-436
+        double lo0 = -1e300, hi0 = 1e300, lo1 = -1e300, hi1 = 1e300;
+        for (int k = j * BS; k < (j + 1) * BS && k < N; k++) {
+            lo0 = fmax(lo0, -p.v_max - ur[2 * k]);
+            hi0 = fmin(hi0, p.v_max - ur[2 * k]);
+            lo1 = fmax(lo1, -p.omega_max - ur[2 * k + 1]);
+            hi1 = fmin(hi1, p.omega_max - ur[2 * k + 1]);
+        }
+        BND(0, j) = lo0; BND(1, j) = hi0; BND(2, j) = lo1; BND(3, j) = hi1;
+    }
+    const double *x0p = a.x0 + 3 * b;
+    const double x0a = th0 + wrap_pi(x0p[2] - th0);                        // :397-401
+    const double d0 = x0p[0] - xr[0], d1 = x0p[1] - xr[1], d2 = x0a - th0;
+    fin = fin && isfinite(d0 + d1 + d2);
+    int it0 = 0;                      // iterations of the previous stage (reported in iters)
+    {
+        const uint32_t *ws = (a.warm && have) ? a.warm + (size_t)t * (N + NB + 1) : nullptr;
+        for (int k = gl; k < N; k += G) HF(k) = (ws && k > 0) ? ws[k] : 0u;
+        for (int j = gl; j < NB; j += G) BF(j) = ws ? ws[N + j] : 0u;
+        if (ws) it0 = (int)ws[N + NB];
+    }
+    __syncthreads();
+
+    GPROF(0);
+    int phase = have ? PH_PDAS : PH_IDLE;
+    if (gany<G>(have && !fin, grp)) {                 // fallback law: the generic kernel owns it
+        if (gl == 0) a.retry[atomicAdd(a.retry_count, 1)] = (int32_t)b;
+        phase = PH_IDLE;
+    }
+
+    // ---- building blocks (all groups run them; `m` masks the LDS writes of the groups
+    // for which the result is meaningful)
+
+    // trajectory under the inputs Z (ZC / ZZ / ZT) -> XS, full objective (constants included,
+    // as the fast kernel's J), and whether any hinge residual exceeds 1e-6 (slack_used, :485)
+    auto objective = [&](int zoff, bool m, int &used) __attribute__((always_inline)) -> double {
+        refresh();
+        double x0 = d0, x1 = d1, x2 = d2;
+#pragma unroll
+        for (int j = 0; j < NB; j++) {
+            const double u0 = base[zoff + 2 * j], u1 = base[zoff + 2 * j + 1];
+#pragma unroll
+            for (int k = j * BS; k < (j + 1) * BS && k < N; k++) {
+                GSTM(XS(k, 0), x0, m); GSTM(XS(k, 1), x1, m); GSTM(XS(k, 2), x2, m);
+                const double n0 = x0 + STG(0, k) * x2 + STG(2, k) * u0;
+                const double n1 = x1 + STG(1, k) * x2 + STG(3, k) * u0;
+                const double n2 = x2 + dt * u1;
+                x0 = n0; x1 = n1; x2 = n2;
+            }
+        }
+        GSTM(XS(N, 0), x0, m); GSTM(XS(N, 1), x1, m); GSTM(XS(N, 2), x2, m);
+        __syncthreads();
+        refresh();
+        double jl = 0.0;
+        int u = 0;
+        for (int k = gl; k <= N; k += G) {
+            const double y0 = XS(k, 0), y1 = XS(k, 1), y2 = XS(k, 2);
+            if (k == N) {
+                jl += P0 * y0 * y0 + P1 * y1 * y1 + P2 * y2 * y2;
+            } else {
+                jl += Q0 * y0 * y0 + Q1 * y1 * y1 + Q2 * y2 * y2;
+                const int j = k / BS;
+                const double uu0 = base[zoff + 2 * j] + STG(4, k), uu1 = base[zoff + 2 * j + 1] + STG(5, k);
+                jl += R0 * uu0 * uu0 + R1 * uu1 * uu1;
+                for (int o = 0; o < no; o++) {
+                    const double r = HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1;
+                    if (r > 0) jl += rho * r * r;
+                    u |= (r > 1e-6);
+                }
+            }
+        }
+        used = gany<G>(u, grp);
+        return gsum<G>(jl);
+    };
+
+    // the quadratic piece of the current sets (HF, BF; fixed components at their bounds):
+    // backward Riccati sweep -> GN; forward sweep -> candidate ZC, trajectory XS, next box
+    // states NBF; row test -> next hinge flags NHF.  Returns "some set would change".
+    auto solve_test = [&]() __attribute__((always_inline)) -> bool {
+        refresh();
+        // per-step stage weights from the active rows (lane-parallel over steps)
+        for (int k = gl; k < N; k += G) {
+            double q00 = Q0, q01 = 0.0, q11 = Q1, qv0 = -Q0 * 0.0, qv1 = -Q1 * 0.0;
+            const uint32_t h = HF(k);
+            if (k > 0 && h) {
+                for (int o = 0; o < no; o++) {
+                    if (!((h >> o) & 1u)) continue;
+                    const double n0 = HN0(o, k), n1 = HN1(o, k), hb = HB(o, k);
+                    q00 += rho * n0 * n0;
+                    q01 += rho * n0 * n1;
+                    q11 += rho * n1 * n1;
+                    qv0 -= rho * hb * n0;
+                    qv1 -= rho * hb * n1;
+                }
+            }
+            WQ(k, 0) = q00; WQ(k, 1) = q01; WQ(k, 2) = q11; WQ(k, 3) = qv0; WQ(k, 4) = qv1;
+        }
+        __syncthreads();
+        GPROF(2);
+        refresh();
+        // backward block Riccati sweep (uniform within the group)
+        RicV<double> V;
+        V.P00 = P0; V.P01 = 0; V.P02 = 0; V.P11 = P1; V.P12 = 0; V.P22 = P2;
+        V.p0 = -P0 * 0.0; V.p1 = -P1 * 0.0; V.p2 = -P2 * 0.0;
+#pragma unroll
+        for (int j = NB - 1; j >= 0; j--) {
+            const int k0 = j * BS, k1 = (k0 + BS < N) ? k0 + BS : N;
+            const uint32_t bfj = BF(j);
+            const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
+            double Gv[8];
+            if constexpr (BS == 1) {
+                V = ric_step1_bf(V, STG(0, j), STG(1, j), STG(2, j), STG(3, j), dt, WQ(j, 0), WQ(j, 1), WQ(j, 2), Q2,
+                                 WQ(j, 3), WQ(j, 4), -Q2 * 0.0, R0, R1, R0 * STG(4, j), R1 * STG(5, j), bf0, bf1,
+                                 bf0 == 1 ? BND(0, j) : BND(1, j), bf1 == 1 ? BND(2, j) : BND(3, j), Gv);
+            } else {
+                RicW<double> W = ric_open(V);
+#pragma unroll
+                for (int k = k1 - 1; k >= k0; k--) {
+                    ric_step(W, STG(0, k), STG(1, k), STG(2, k), STG(3, k), dt, WQ(k, 0), WQ(k, 1), WQ(k, 2), Q2,
+                             WQ(k, 3), WQ(k, 4), -Q2 * 0.0, R0, R1, R0 * STG(4, k), R1 * STG(5, k));
+                }
+                V = ric_block_bf(W, bf0, bf1, bf0 == 1 ? BND(0, j) : BND(1, j), bf1 == 1 ? BND(2, j) : BND(3, j), Gv);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) GST(GN(j, q), Gv[q]);
+        }
+        __syncthreads();
+        GPROF(3);
+        refresh();
+        // forward sweep: inputs (free: gains; fixed: bound), box rule on the value (free) or
+        // the multiplier (fixed), trajectory
+        bool bchg = false;
+        double x0 = d0, x1 = d1, x2 = d2;
+#pragma unroll
+        for (int j = 0; j < NB; j++) {
+            const double lo0 = BND(0, j), hi0 = BND(1, j), lo1 = BND(2, j), hi1 = BND(3, j);
+            const double e0 = GN(j, 0) * x0 + GN(j, 1) * x1 + GN(j, 2) * x2 + GN(j, 6);
+            const double e1 = GN(j, 3) * x0 + GN(j, 4) * x1 + GN(j, 5) * x2 + GN(j, 7);
+            const uint32_t bfj = BF(j);
+            const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
+            const double u0v = bf0 == 0 ? e0 : (bf0 == 1 ? lo0 : hi0);
+            const double u1v = bf1 == 0 ? e1 : (bf1 == 1 ? lo1 : hi1);
+            const int ns0 = box_rule_bf(bf0, e0, lo0, hi0, eps_b), ns1 = box_rule_bf(bf1, e1, lo1, hi1, eps_b);
+            bchg = bchg || ns0 != bf0 || ns1 != bf1;
+            *(gl == 0 ? &NBF(j) : reinterpret_cast<uint32_t *>(junk)) = (uint32_t)(ns0 | (ns1 << 2));
+            GST(ZC(2 * j), u0v);
+            GST(ZC(2 * j + 1), u1v);
+#pragma unroll
+            for (int k = j * BS; k < (j + 1) * BS && k < N; k++) {
+                GST(XS(k, 0), x0); GST(XS(k, 1), x1); GST(XS(k, 2), x2);
+                const double n0 = x0 + STG(0, k) * x2 + STG(2, k) * u0v;
+                const double n1 = x1 + STG(1, k) * x2 + STG(3, k) * u0v;
+                const double n2 = x2 + dt * u1v;
+                x0 = n0; x1 = n1; x2 = n2;
+            }
+        }
+        GST(XS(N, 0), x0); GST(XS(N, 1), x1); GST(XS(N, 2), x2);
+        __syncthreads();
+        GPROF(4);
+        refresh();
+        // hinge rule per row (lane-parallel over steps)
+        bool hchg = false;
+        for (int k = gl; k < N; k += G) {
+            const uint32_t h = HF(k);
+            uint32_t nh = h;
+            if (k > 0) {
+                const double y0 = XS(k, 0), y1 = XS(k, 1);
+                for (int o = 0; o < no; o++) {
+                    const double r = HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1;
+                    const uint32_t act = (h >> o) & 1u;
+                    const uint32_t na = act ? (r > -eps_h) : (r > eps_h);
+                    nh ^= (na ^ act) << o;
+                }
+            }
+            NHF(k) = nh;
+            hchg = hchg || nh != h;
+        }
+        const bool chg = gany<G>(bchg || hchg, grp);
+        __syncthreads();
+        GPROF(5);
+        return chg;
+    };
+
+    // gradient of the objective at ZZ (whose trajectory is in XS): hinge forces per step
+    // (lane-parallel), then the adjoint recursion (uniform) -> GR
+    auto gradient = [&](bool m) __attribute__((always_inline)) {
+        refresh();
+        for (int k = gl; k < N; k += G) {
+            double f0 = 0.0, f1 = 0.0;
+            if (k > 0) {
+                const double y0 = XS(k, 0), y1 = XS(k, 1);
+                for (int o = 0; o < no; o++) {
+                    const double r = HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1;
+                    if (r > 0) {
+                        f0 -= 2 * rho * r * HN0(o, k);
+                        f1 -= 2 * rho * r * HN1(o, k);
+                    }
+                }
+            }
+            if (m) { FR(0, k) = f0; FR(1, k) = f1; }
+        }
+        __syncthreads();
+        refresh();
+        double l0 = 2 * P0 * XS(N, 0), l1 = 2 * P1 * XS(N, 1), l2 = 2 * P2 * XS(N, 2);
+#pragma unroll
+        for (int j = NB - 1; j >= 0; j--) {
+            double g0 = 0.0, g1 = 0.0;
+            const double z0 = ZZ(2 * j), z1 = ZZ(2 * j + 1);
+#pragma unroll
+            for (int k = ((j + 1) * BS < N ? (j + 1) * BS : N) - 1; k >= j * BS; k--) {
+                g0 += STG(2, k) * l0 + STG(3, k) * l1 + 2 * R0 * (z0 + STG(4, k));
+                g1 += dt * l2 + 2 * R1 * (z1 + STG(5, k));
+                const double m0 = 2 * Q0 * XS(k, 0) + l0 + (k > 0 ? FR(0, k) : 0.0);
+                const double m1 = 2 * Q1 * XS(k, 1) + l1 + (k > 0 ? FR(1, k) : 0.0);
+                const double m2 = 2 * Q2 * XS(k, 2) + STG(0, k) * l0 + STG(1, k) * l1 + l2;
+                l0 = m0; l1 = m1; l2 = m2;
+            }
+            GSTM(GR(2 * j), g0, m); GSTM(GR(2 * j + 1), g1, m);
+        }
+        __syncthreads();
+    };
+
+    // ---- the iteration loop (groups in lockstep)
+    int it = 0, cyc = 0;
+    double F = 0.0;
+    uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    const int max_iter = p.max_iter;
+    while (__any(phase <= PH_PN)) {
+        const bool act = phase <= PH_PN;
+        const bool pn = phase == PH_PN;
+        if (__any(pn)) {
+            // projected Newton: gradient at z, epsilon-active box components, hinge rows with
+            // r > 0 -- the sets of this solve (rmpc_mpc_dense.hip phase 2)
+            gradient(pn);
+            refresh();
+            double wl = 0.0;
+            for (int i = gl; i < 2 * NB; i += G) {
+                const int j = i >> 1, c = i & 1;
+                const double lo = BND(2 * c, j), hi = BND(2 * c + 1, j), z = ZZ(i);
+                wl = fmax(wl, fabs(z - clampv(z - GR(i), lo, hi)));
+            }
+            const double eps = fmin(1e-6, gmaxv<G>(wl));
+            if (pn) {
+                for (int j = gl; j < NB; j += G) {
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int c = 0; c < 2; c++) {
+                        const double lo = BND(2 * c, j), hi = BND(2 * c + 1, j), z = ZZ(2 * j + c), g = GR(2 * j + c);
+                        const uint32_t s = (z <= lo + eps && g > 0) ? 1u : ((z >= hi - eps && g < 0) ? 2u : 0u);
+                        w |= s << (2 * c);
+                    }
+                    BF(j) = w;
+                }
+                for (int k = gl; k < N; k += G) {
+                    uint32_t nh = 0;
+                    if (k > 0) {
+                        const double y0 = XS(k, 0), y1 = XS(k, 1);
+                        for (int o = 0; o < no; o++)
+                            if (HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1 > 0) nh |= 1u << o;
+                    }
+                    HF(k) = nh;
+                }
+            }
+            __syncthreads();
+            GPROF(1);
+        }
+        if (act) it++;
+        const bool chg = solve_test();
+        const bool cert = act && !chg;
+        if (__any(cert)) {
+            // ---- outputs from the certified candidate (mpc_controller.py:484-520)
+            int used = 0;
+            const double J = objective(RC::ZC, cert, used);
+            refresh();
+            if (cert && isfinite(J)) {
+                const int sc = a.step_count ? a.step_count[b] : 0;
+                for (int k = gl; k < N; k += G) {
+                    const int j = k / BS;
+                    const double v0 = ZC(2 * j) + STG(4, k);
+                    double v1 = ZC(2 * j + 1) + STG(5, k);
+                    if (k == 0 && sc < p.ramp_up_steps) {                      // :502-505
+                        const double lim = p.omega_max * ((double)(sc + 1) / (double)p.ramp_up_steps);
+                        v1 = clampv(v1, -lim, lim);
+                    }
+                    if (a.u_seq) {
+                        a.u_seq[((size_t)b * N + k) * 2] = v0;
+                        a.u_seq[((size_t)b * N + k) * 2 + 1] = v1;
+                    }
+                    if (k == 0) {
+                        a.u0[2 * b] = v0;
+                        a.u0[2 * b + 1] = v1;
+                    }
+                }
+                if (a.x_pred) {                                                 // :497
+                    for (int k = gl; k <= N; k += G) {
+                        double *xp = a.x_pred + ((size_t)b * (N + 1) + k) * 3;
+                        xp[0] = XS(k, 0) + xr[3 * k];
+                        xp[1] = XS(k, 1) + xr[3 * k + 1];
+                        xp[2] = XS(k, 2) + xr[3 * k + 2];
+                    }
+                }
+                if (gl == 0) {
+                    if (a.step_count) a.step_count[b] = sc + 1;                 // :507
+                    if (a.cost) a.cost[b] = J;
+                    if (a.slack_used) a.slack_used[b] = (uint8_t)used;
+                    a.status[b] = RMPC_OPTIMAL;
+                    if (a.iters) a.iters[b] = it0 + it;
+                }
+            } else if (cert && gl == 0) {
+                a.retry[atomicAdd(a.retry_count, 1)] = (int32_t)b;
+            }
+            __syncthreads();
+            GPROF(6);
+        }
+        if (cert) phase = PH_DONE;
+        // PDAS groups: take the new sets; cycle / cap -> projected Newton
+        bool to_pn = false, fail = false;
+        if (phase == PH_PDAS) {
+            refresh();
+            for (int k = gl; k < N; k += G) HF(k) = NHF(k);
+            for (int j = gl; j < NB; j += G) BF(j) = NBF(j);
+            if (a.pdas_cap > 4) {
+                uint64_t sig = 1469598103934665603ull;
+                for (int k = 0; k < N; k++) sig = (sig ^ (uint64_t)NHF(k)) * 1099511628211ull;
+                for (int j = 0; j < NB; j++) sig = (sig ^ (uint64_t)NBF(j)) * 1099511628211ull;
+                if (sig == s0 || sig == s1 || sig == s2 || sig == s3) cyc = 1;
+                s3 = s2; s2 = s1; s1 = s0; s0 = sig;
+            }
+            if (it >= a.pdas_cap || cyc) {
+                if (it < max_iter) to_pn = true;
+                else fail = true;
+            }
+        }
+        __syncthreads();
+        if (__any(to_pn)) {          // z = projected last candidate, F = objective(z)
+            refresh();
+            if (to_pn) {
+                for (int i = gl; i < 2 * NB; i += G) {
+                    const int j = i >> 1, c = i & 1;
+                    ZZ(i) = clampv(ZC(i), BND(2 * c, j), BND(2 * c + 1, j));
+                }
+            }
+            __syncthreads();
+            int u;
+            const double f = objective(RC::ZZ, to_pn, u);
+            if (to_pn) { F = f; phase = PH_PN; }
+            __syncthreads();
+        }
+        GPROF(7);
+        // projected-Newton groups that did not certify: Armijo along the projection arc
+        bool searching = pn && !cert;
+        if (__any(searching)) {
+            refresh();
+            double alpha = 1.0;
+            for (int ls = 0; ls < 40 && __any(searching); ls++) {
+                double gd = 0.0;
+                for (int i = gl; i < 2 * NB; i += G) {
+                    const int j = i >> 1, c = i & 1;
+                    const double z = ZZ(i);
+                    const double zt = clampv(z + alpha * (ZC(i) - z), BND(2 * c, j), BND(2 * c + 1, j));
+                    if (searching) ZT(i) = zt;
+                    gd += GR(i) * (zt - z);
+                }
+                gd = gsum<G>(gd);
+                __syncthreads();
+                int u;
+                const double Ft = objective(RC::ZT, searching, u);
+                refresh();
+                const bool acc = searching && Ft <= F + 1e-4 * gd;
+                if (acc) {
+                    for (int i = gl; i < 2 * NB; i += G) ZZ(i) = ZT(i);
+                    F = Ft;
+                    searching = false;
+                }
+                alpha *= 0.5;
+                __syncthreads();
+            }
+            if (searching) fail = true;          // no acceptable step
+            GPROF(8);
+        }
+        if (prof_on) pacc[9]++;
+        if (phase == PH_PN && !cert && it >= max_iter) fail = true;
+        if (fail) {
+            if (gl == 0) a.retry[atomicAdd(a.retry_count, 1)] = (int32_t)b;
+            phase = PH_IDLE;
+        }
+    }
+    if (prof_on && gl == 0 && grp == 0) {
+        for (int q = 0; q < 10; q++) atomicAdd(a.prof + q, pacc[q]);
+        atomicAdd(a.prof + 10, 1ull);
+    }
+#undef STG
+#undef BND
+#undef HN0
+#undef HN1
+#undef HB
+#undef WQ
+#undef GN
+#undef XS
+#undef ZC
+#undef ZZ
+#undef ZT
+#undef GR
+#undef FR
+#undef HF
+#undef BF
+#undef NHF
+#undef NBF
+#undef GST
+#undef GSTM
+}
+
+// Persistent over rounds of 64/G list entries per wave; one wave per workgroup.
+template <int N, int BS, int G>
+__global__ __launch_bounds__(64, 1) void mpc_group_kernel(GroupArgs a) {
+    constexpr int NB = (N + BS - 1) / BS, RPW = 64 / G;
+    extern __shared__ double lds[];
+    const int lane = threadIdx.x, gl = lane % G, grp = lane / G;
+    const int rec = GRec<N, NB>::size(a.no);
+    const int cnt = *a.count;
+    for (int t0 = blockIdx.x * RPW; t0 < cnt; t0 += gridDim.x * RPW) {
+        const int t = t0 + grp;
+        group_solve<N, BS, G>(a, lds + grp * rec, t, t < cnt, gl, grp);
+        __syncthreads();
+    }
+}
+
+// lanes per robot: 16 (four robots per wave) while the record leaves room for four waves
+// per CU, else 32
+static int group_lanes(int N, int bs) { return N > 20 ? 32 : 16; }
+
+static int group_rec(int N, int bs, int no) {
+    if (bs == 2 && N == 6) return GRec<6, 3>::size(no);
+    switch (N) {
+        case 6: return GRec<6, 6>::size(no);
+        case 10: return GRec<10, 10>::size(no);
+        case 20: return GRec<20, 20>::size(no);
+        default: return GRec<30, 30>::size(no);
+    }
+}
+
+}  // namespace rmpc
+
+using namespace rmpc;
+
+bool rmpc_mpc_group_supported(int N, int bs, int no) {
+    const bool inst = (bs == 1 && (N == 6 || N == 10 || N == 20 || N == 30)) || (bs == 2 && N == 6);
+    if (!inst || no > 16) return false;
+    const size_t lds = (size_t)(64 / group_lanes(N, bs)) * group_rec(N, bs, no) * sizeof(double);
+    return lds <= 160 * 1024;
+}
+
+hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no, int64_t capacity,
+                                 const double *x0, const double *x_refs, int ref_rows,
+                                 const double *u_refs, int uref_rows, const double *obstacles,
+                                 int32_t *step_count, double *u0, double *u_seq, double *x_pred,
+                                 double *cost, int32_t *status, uint8_t *slack_used, int32_t *iters,
+                                 const int32_t *index, const int32_t *count, int32_t *retry,
+                                 int32_t *retry_count, int pdas_cap, const uint32_t *warm,
+                                 hipStream_t stream, unsigned long long *prof) {
+    if (capacity <= 0) return hipSuccess;
+    if (!rmpc_mpc_group_supported(N, bs, no)) return hipErrorInvalidValue;
+    GroupArgs a;
+    a.prm = prm;
+    a.no = no;
+    a.x0 = x0; a.x_refs = x_refs; a.u_refs = u_refs; a.obs = obstacles;
+    a.ref_rows = ref_rows; a.uref_rows = uref_rows;
+    a.step_count = step_count;
+    a.u0 = u0; a.u_seq = u_seq; a.x_pred = x_pred; a.cost = cost;
+    a.status = status; a.iters = iters; a.slack_used = slack_used;
+    a.index = index; a.count = count; a.retry = retry; a.retry_count = retry_count;
+    a.warm = warm;
+    a.prof = prof;
+    a.pdas_cap = pdas_cap < RMPC_PDAS_ITERS ? pdas_cap : RMPC_PDAS_ITERS;
+    const int G = group_lanes(N, bs), rpw = 64 / G;
+    const size_t lds = (size_t)rpw * group_rec(N, bs, no) * sizeof(double);
+    const int per_cu = getenv("RMPC_GROUP_WPC") ? atoi(getenv("RMPC_GROUP_WPC")) : 4;
+    const int64_t gmax = (int64_t)256 * (per_cu > 0 ? per_cu : 4);
+    const int64_t need = (capacity + rpw - 1) / rpw;
+    const dim3 g((unsigned)(need < gmax ? need : gmax)), blk(64);
+    const void *fn = (bs == 1 && N == 30)   ? (const void *)mpc_group_kernel<30, 1, 32>
+                     : (bs == 1 && N == 20) ? (const void *)mpc_group_kernel<20, 1, 16>
+                     : (bs == 1 && N == 10) ? (const void *)mpc_group_kernel<10, 1, 16>
+                     : (bs == 1 && N == 6)  ? (const void *)mpc_group_kernel<6, 1, 16>
+                                            : (const void *)mpc_group_kernel<6, 2, 16>;
+    if (lds > 64 * 1024) {
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    if (bs == 1 && N == 30) hipLaunchKernelGGL((mpc_group_kernel<30, 1, 32>), g, blk, lds, stream, a);
+    else if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_group_kernel<20, 1, 16>), g, blk, lds, stream, a);
+    else if (bs == 1 && N == 10) hipLaunchKernelGGL((mpc_group_kernel<10, 1, 16>), g, blk, lds, stream, a);
+    else if (bs == 1 && N == 6) hipLaunchKernelGGL((mpc_group_kernel<6, 1, 16>), g, blk, lds, stream, a);
+    else hipLaunchKernelGGL((mpc_group_kernel<6, 2, 16>), g, blk, lds, stream, a);
+    return hipGetLastError();
+}
