@@ -308,9 +308,9 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         a.count = count;
         a.retry = (int32_t *)c->retry.p;
         a.retry_count = (int32_t *)c->retry_count.p;
-        // default cap: 10 at N <= 20 (tuned on BASELINE config 3), 16 beyond (config 4, where a
-        // dense-tail iteration at n = 60 costs ~2x a lane-per-robot one)
-        a.pdas_cap = getenv("RMPC_FAST_CAP") ? atoi(getenv("RMPC_FAST_CAP")) : (p->horizon <= 20 ? 10 : 16);
+        // default cap (sweeps with the lane-group tail): 7 at N <= 20 (BASELINE config 3), 12
+        // beyond (config 4)
+        a.pdas_cap = getenv("RMPC_FAST_CAP") ? atoi(getenv("RMPC_FAST_CAP")) : (p->horizon <= 20 ? 7 : 12);
         const bool warm = !getenv("RMPC_COLD_TAIL");
         if (warm) {
             HIP_TRY(c->retry_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));

@@ -234,17 +234,27 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
     auto objective = [&](int zoff, bool m, int &used) __attribute__((always_inline)) -> double {
         refresh();
         double x0 = d0, x1 = d1, x2 = d2;
+        // per step: inputs of its block + linearisation, step k+1's loaded while k computes
+        double nx[6];
+        auto ldo = [&](int k) __attribute__((always_inline)) {
+            nx[0] = base[zoff + 2 * (k / BS)];
+            nx[1] = base[zoff + 2 * (k / BS) + 1];
 #pragma unroll
-        for (int j = 0; j < NB; j++) {
-            const double u0 = base[zoff + 2 * j], u1 = base[zoff + 2 * j + 1];
+            for (int f = 0; f < 4; f++) nx[2 + f] = STG(f, k);
+        };
+        ldo(0);
 #pragma unroll
-            for (int k = j * BS; k < (j + 1) * BS && k < N; k++) {
-                GSTM(XS(k, 0), x0, m); GSTM(XS(k, 1), x1, m); GSTM(XS(k, 2), x2, m);
-                const double n0 = x0 + STG(0, k) * x2 + STG(2, k) * u0;
-                const double n1 = x1 + STG(1, k) * x2 + STG(3, k) * u0;
-                const double n2 = x2 + dt * u1;
-                x0 = n0; x1 = n1; x2 = n2;
-            }
+        for (int k = 0; k < N; k++) {
+            double c[6];
+#pragma unroll
+            for (int f = 0; f < 6; f++) c[f] = nx[f];
+            if (k + 1 < N) ldo(k + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            GSTM(XS(k, 0), x0, m); GSTM(XS(k, 1), x1, m); GSTM(XS(k, 2), x2, m);
+            const double n0 = x0 + c[2] * x2 + c[4] * c[0];
+            const double n1 = x1 + c[3] * x2 + c[5] * c[0];
+            const double n2 = x2 + dt * c[1];
+            x0 = n0; x1 = n1; x2 = n2;
         }
         GSTM(XS(N, 0), x0, m); GSTM(XS(N, 1), x1, m); GSTM(XS(N, 2), x2, m);
         __syncthreads();
@@ -300,17 +310,41 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
         RicV<double> V;
         V.P00 = P0; V.P01 = 0; V.P02 = 0; V.P11 = P1; V.P12 = 0; V.P22 = P2;
         V.p0 = -P0 * 0.0; V.p1 = -P1 * 0.0; V.p2 = -P2 * 0.0;
+        if constexpr (BS == 1) {
+            // single-step blocks, software-pipelined: step j-1's record is loaded while step j
+            // computes (the scheduler does not hoist LDS loads across unrolled steps itself)
+            double nx[16];
+            uint32_t nbf = 0;
+            auto ld = [&](int j) __attribute__((always_inline)) {
 #pragma unroll
-        for (int j = NB - 1; j >= 0; j--) {
-            const int k0 = j * BS, k1 = (k0 + BS < N) ? k0 + BS : N;
-            const uint32_t bfj = BF(j);
-            const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
-            double Gv[8];
-            if constexpr (BS == 1) {
-                V = ric_step1_bf(V, STG(0, j), STG(1, j), STG(2, j), STG(3, j), dt, WQ(j, 0), WQ(j, 1), WQ(j, 2), Q2,
-                                 WQ(j, 3), WQ(j, 4), -Q2 * 0.0, R0, R1, R0 * STG(4, j), R1 * STG(5, j), bf0, bf1,
-                                 bf0 == 1 ? BND(0, j) : BND(1, j), bf1 == 1 ? BND(2, j) : BND(3, j), Gv);
-            } else {
+                for (int f = 0; f < 12; f++) nx[f] = base[RC::STEP + 12 * j + f];
+#pragma unroll
+                for (int f = 0; f < 4; f++) nx[12 + f] = base[RC::BLK + 12 * j + f];
+                nbf = BF(j);
+            };
+            ld(NB - 1);
+#pragma unroll
+            for (int j = NB - 1; j >= 0; j--) {
+                double c[16];
+#pragma unroll
+                for (int f = 0; f < 16; f++) c[f] = nx[f];
+                const uint32_t bfj = nbf;
+                if (j > 0) ld(j - 1);
+                __builtin_amdgcn_sched_barrier(0);
+                const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
+                double Gv[8];
+                V = ric_step1_bf(V, c[0], c[1], c[2], c[3], dt, c[6], c[7], c[8], Q2, c[9], c[10], -Q2 * 0.0, R0, R1,
+                                 R0 * c[4], R1 * c[5], bf0, bf1, bf0 == 1 ? c[12] : c[13], bf1 == 1 ? c[14] : c[15], Gv);
+#pragma unroll
+                for (int q = 0; q < 8; q++) GST(GN(j, q), Gv[q]);
+            }
+        } else {
+#pragma unroll
+            for (int j = NB - 1; j >= 0; j--) {
+                const int k0 = j * BS, k1 = (k0 + BS < N) ? k0 + BS : N;
+                const uint32_t bfj = BF(j);
+                const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
+                double Gv[8];
                 RicW<double> W = ric_open(V);
 #pragma unroll
                 for (int k = k1 - 1; k >= k0; k--) {
@@ -318,9 +352,9 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
                              WQ(k, 3), WQ(k, 4), -Q2 * 0.0, R0, R1, R0 * STG(4, k), R1 * STG(5, k));
                 }
                 V = ric_block_bf(W, bf0, bf1, bf0 == 1 ? BND(0, j) : BND(1, j), bf1 == 1 ? BND(2, j) : BND(3, j), Gv);
-            }
 #pragma unroll
-            for (int q = 0; q < 8; q++) GST(GN(j, q), Gv[q]);
+                for (int q = 0; q < 8; q++) GST(GN(j, q), Gv[q]);
+            }
         }
         __syncthreads();
         GPROF(3);
@@ -329,12 +363,28 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
         // the multiplier (fixed), trajectory
         bool bchg = false;
         double x0 = d0, x1 = d1, x2 = d2;
+        // block record (bounds + gains) and step data of block j+1 loaded while j computes
+        double nx[16];
+        uint32_t nbf = 0;
+        auto ldf = [&](int j) __attribute__((always_inline)) {
+#pragma unroll
+            for (int f = 0; f < 12; f++) nx[f] = base[RC::BLK + 12 * j + f];
+#pragma unroll
+            for (int f = 0; f < 4; f++) nx[12 + f] = BS == 1 ? base[RC::STEP + 12 * j + f] : 0.0;
+            nbf = BF(j);
+        };
+        ldf(0);
 #pragma unroll
         for (int j = 0; j < NB; j++) {
-            const double lo0 = BND(0, j), hi0 = BND(1, j), lo1 = BND(2, j), hi1 = BND(3, j);
-            const double e0 = GN(j, 0) * x0 + GN(j, 1) * x1 + GN(j, 2) * x2 + GN(j, 6);
-            const double e1 = GN(j, 3) * x0 + GN(j, 4) * x1 + GN(j, 5) * x2 + GN(j, 7);
-            const uint32_t bfj = BF(j);
+            double c[16];
+#pragma unroll
+            for (int f = 0; f < 16; f++) c[f] = nx[f];
+            const uint32_t bfj = nbf;
+            if (j + 1 < NB) ldf(j + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            const double lo0 = c[0], hi0 = c[1], lo1 = c[2], hi1 = c[3];
+            const double e0 = c[4] * x0 + c[5] * x1 + c[6] * x2 + c[10];
+            const double e1 = c[7] * x0 + c[8] * x1 + c[9] * x2 + c[11];
             const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
             const double u0v = bf0 == 0 ? e0 : (bf0 == 1 ? lo0 : hi0);
             const double u1v = bf1 == 0 ? e1 : (bf1 == 1 ? lo1 : hi1);
@@ -346,8 +396,10 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
 #pragma unroll
             for (int k = j * BS; k < (j + 1) * BS && k < N; k++) {
                 GST(XS(k, 0), x0); GST(XS(k, 1), x1); GST(XS(k, 2), x2);
-                const double n0 = x0 + STG(0, k) * x2 + STG(2, k) * u0v;
-                const double n1 = x1 + STG(1, k) * x2 + STG(3, k) * u0v;
+                const double sa0 = BS == 1 ? c[12] : STG(0, k), sa1 = BS == 1 ? c[13] : STG(1, k);
+                const double sb0 = BS == 1 ? c[14] : STG(2, k), sb1 = BS == 1 ? c[15] : STG(3, k);
+                const double n0 = x0 + sa0 * x2 + sb0 * u0v;
+                const double n1 = x1 + sa1 * x2 + sb1 * u0v;
                 const double n2 = x2 + dt * u1v;
                 x0 = n0; x1 = n1; x2 = n2;
             }

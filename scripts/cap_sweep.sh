@@ -1,0 +1,9 @@
+#!/bin/bash
+# fast-stage cap sweep: bench CONFIG with each env setting, print value + stage split
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+cfg=$1; shift
+for v in "$@"; do
+  [ "$v" = "-" ] && v=""
+  env $v timeout -k 10 300 python bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/cs.json 2>gpurun_out/cs.err || exit $?
+  python -c "import json;d=json.load(open('gpurun_out/cs.json'));r=d['roofline'];print('$cfg [$v] value %.3e ms %.3f'%(d['value'],d['ms_per_step']), {k:round(v,3) for k,v in (r.get('stage_ms') or {}).items()})"
+done
