@@ -356,6 +356,9 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                         "out %.0f upd %.0f ls %.0f | per loop-it: weights %.0f back %.0f fwd %.0f rows %.0f\n",
                         cn[0], cn[8], h[10], h[9] / r, h[0] / r, h[1] / r, h[6] / r, h[7] / r, h[8] / r,
                         h[2] / li, h[3] / li, h[4] / li, h[5] / li);
+                fprintf(stderr, "[group] tail iterations per robot:");
+                for (int q = 0; q < 32; q++) fprintf(stderr, " %llu", h[24 + q]);
+                fprintf(stderr, "\n");
                 const double w = h[20] ? (double)h[20] : 1.0;
                 fprintf(stderr, "[fast] waves=%llu per wave: total %.0f back %.0f fwd %.0f iters %.2f | per iter: back %.0f fwd %.0f\n",
                         h[20], h[19] / w, h[16] / w, h[17] / w, h[18] / w, h[16] / (double)(h[18] ? h[18] : 1),

@@ -126,11 +126,15 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     // Obstacles (x, y, d_safe + r) staged in LDS once: read from global inside the sweeps
     // they compile to vector loads (the pointer may alias the kernel's stores) whose
     // vmcnt(0) waits would drain the gain prefetch at every step.
-    __shared__ T obs_s[3 * RMPC_MAX_OBSTACLES];
+    __shared__ T obs_s[3 * (RMPC_MAX_OBSTACLES + 1)];
     if (lane < a.no) {
         obs_s[3 * lane] = (T)a.obs[3 * lane];
         obs_s[3 * lane + 1] = (T)a.obs[3 * lane + 1];
         obs_s[3 * lane + 2] = (T)(a.prm.d_safe + a.obs[3 * lane + 2]);
+    } else if (lane <= RMPC_MAX_OBSTACLES) {   // the rows' one-ahead prefetch reads slot no
+        obs_s[3 * lane] = (T)0;
+        obs_s[3 * lane + 1] = (T)0;
+        obs_s[3 * lane + 2] = (T)0;
     }
     __syncthreads();
     const int64_t t = (int64_t)blockIdx.x * RMPC_WAVE + lane;
@@ -222,9 +226,14 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                 T q00 = Q0, q01 = 0, q11 = Q1;
                 T qv0 = -Q0 * (T)0, qv1 = -Q1 * (T)0, qv2 = -Q2 * (T)0;
                 if (k > 0 && Hf[k]) {
+                    const T px = PX(k), py = PY(k);
+                    T cx = obs_s[0], cy = obs_s[1], cs = obs_s[2];
                     for (int o = 0; o < no; o++) {      // branch-free: inactive rows add 0
+                        // obstacle o+1 loads while row o computes (LDS latency off the row chain)
+                        const T nx = obs_s[3 * o + 3], ny = obs_s[3 * o + 4], ns = obs_s[3 * o + 5];
                         T n0, n1, hb;
-                        hinge_row_fast(PX(k), PY(k), obs_s[3 * o], obs_s[3 * o + 1], obs_s[3 * o + 2], n0, n1, hb);
+                        hinge_row_fast(px, py, cx, cy, cs, n0, n1, hb);
+                        cx = nx; cy = ny; cs = ns;
                         const T w = ((Hf[k] >> o) & 1u) ? rho : (T)0;
                         q00 += w * n0 * n0;
                         q01 += w * n0 * n1;
@@ -249,9 +258,13 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                     T q00 = Q0, q01 = 0, q11 = Q1;
                     T qv0 = -Q0 * (T)0, qv1 = -Q1 * (T)0, qv2 = -Q2 * (T)0;
                     if (k > 0 && Hf[k]) {
+                        const T px = PX(k), py = PY(k);
+                        T cx = obs_s[0], cy = obs_s[1], cs = obs_s[2];
                         for (int o = 0; o < no; o++) {      // branch-free: inactive rows add 0
+                            const T nx = obs_s[3 * o + 3], ny = obs_s[3 * o + 4], ns = obs_s[3 * o + 5];
                             T n0, n1, hb;
-                            hinge_row_fast(PX(k), PY(k), obs_s[3 * o], obs_s[3 * o + 1], obs_s[3 * o + 2], n0, n1, hb);
+                            hinge_row_fast(px, py, cx, cy, cs, n0, n1, hb);
+                            cx = nx; cy = ny; cs = ns;
                             const T w = ((Hf[k] >> o) & 1u) ? rho : (T)0;
                             q00 += w * n0 * n0;
                             q01 += w * n0 * n1;
@@ -330,9 +343,13 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                 const T uu0 = u0v + V0[k], uu1 = u1v + V1(k);
                 J += R0 * uu0 * uu0 + R1 * uu1 * uu1;
                 uint32_t hk = Hf[k];
+                const T px = PX(k), py = PY(k);
+                T cx = obs_s[0], cy = obs_s[1], cs = obs_s[2];
                 for (int o = 0; o < no; o++) {          // branch-free row update
+                    const T nx = obs_s[3 * o + 3], ny = obs_s[3 * o + 4], ns = obs_s[3 * o + 5];
                     T n0, n1, hb;
-                    const bool kept = hinge_row_fast(PX(k), PY(k), obs_s[3 * o], obs_s[3 * o + 1], obs_s[3 * o + 2], n0, n1, hb);
+                    const bool kept = hinge_row_fast(px, py, cx, cy, cs, n0, n1, hb);
+                    cx = nx; cy = ny; cs = ns;
                     const T r = kept ? hb - n0 * x0 - n1 * x1 : (T)-1;   // unkept: never active
                     const T rp = fmax(r, (T)0);
                     J += rho * rp * rp;

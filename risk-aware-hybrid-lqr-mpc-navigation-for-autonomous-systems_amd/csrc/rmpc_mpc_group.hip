@@ -634,6 +634,8 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
             if (gl == 0) a.retry[atomicAdd(a.retry_count, 1)] = (int32_t)b;
             phase = PH_IDLE;
         }
+        if (prof_on && gl == 0 && (cert || fail))   // per robot: tail iterations (histogram)
+            atomicAdd(a.prof + 24 + min(it, 31), 1ull);
     }
     if (prof_on && gl == 0 && grp == 0) {
         for (int q = 0; q < 10; q++) atomicAdd(a.prof + q, pacc[q]);
