@@ -18,6 +18,7 @@ for f in sorted(glob.glob(tag + "_p*/**/*counter_collection.csv", recursive=True
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
         key = ("fast" if "mpc_ltv_fast_kernel" in name else "dense" if "mpc_dense_kernel" in name
+               else "group" if "mpc_group_kernel" in name
                else "generic" if "mpc_solve_kernel" in name else None)
         if key and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE"):
             vals[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
