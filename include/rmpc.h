@@ -75,7 +75,8 @@ typedef struct RmpcMpcParams {
     int32_t horizon;       /* N (mpc_controller.py:111)                            */
     int32_t block_size;    /* move blocking, LTV only (:118-121)                    */
     int32_t formulation;   /* RMPC_LTV / RMPC_LTI                                   */
-    int32_t soft;          /* use_soft_constraints (default 1)                      */
+    int32_t soft;          /* use_soft_constraints (default 1; 0 = hard half-spaces,
+                              :383-386, infeasible -> RMPC_FALLBACK)               */
     int32_t precision;     /* RMPC_F64 / RMPC_F32                                   */
     int32_t max_iter;      /* active-set iteration cap (<=0: default 64)            */
     int32_t ramp_up_steps; /* cold-start omega ramp length (:144, default 10)       */

@@ -87,8 +87,16 @@ def solve_qp(H, c, E, f, G, h, max_iter=100, tol=1e-11, polish=True):
             dz = (rc - z * dt) / t if p else np.zeros(0)
             return dw, -ndy, dt, dz
 
-        # predictor
-        dw, dy, dt, dz = direction(-t * z)
+        # predictor.  A diverging iterate (infeasible QP: CVXPY reports "infeasible" and the
+        # reference falls back, mpc_controller.py:521-522) ends the loop without "optimal".
+        if not (np.all(np.isfinite(w)) and np.abs(w).max(initial=0) < 1e12):
+            status = "infeasible"
+            break
+        try:
+            dw, dy, dt, dz = direction(-t * z)
+        except np.linalg.LinAlgError:
+            status = "infeasible"
+            break
 
         def step(v, dv):
             neg = dv < 0
@@ -105,7 +113,11 @@ def solve_qp(H, c, E, f, G, h, max_iter=100, tol=1e-11, polish=True):
             # iterates centred; plain Mehrotra stalls on some slack-heavy instances)
             if resn / res0 > 10.0 * mu / mu0:
                 sigma = max(sigma, 0.5)
-            dw, dy, dt, dz = direction(-t * z + sigma * mu - dt * dz)
+            try:
+                dw, dy, dt, dz = direction(-t * z + sigma * mu - dt * dz)
+            except np.linalg.LinAlgError:
+                status = "infeasible"
+                break
             ap = 0.995 * step(t, dt)
             ad = 0.995 * step(z, dz)
             a = min(ap, ad)
@@ -137,6 +149,10 @@ def solve_qp(H, c, E, f, G, h, max_iter=100, tol=1e-11, polish=True):
         wp, lam = _kkt_solve(H, C, -c, d)
         lam = -lam
         if not np.all(np.isfinite(wp)):
+            break
+        # an inconsistent active set (e.g. a violated row on the fixed initial state of an
+        # infeasible hard-constrained QP) has no exact KKT point: lstsq must not pass for one
+        if C.shape[0] and np.abs(C @ wp - d).max() > 1e-9 * (1.0 + np.abs(d).max()):
             break
         if not p:
             res.w, res.polished, res.status = wp, True, "optimal"

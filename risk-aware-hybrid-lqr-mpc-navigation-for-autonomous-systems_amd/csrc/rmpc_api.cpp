@@ -190,8 +190,6 @@ static int check_mpc_params(const RmpcMpcParams *p, int ref_rows, int uref_rows,
         if (uref_rows < N) return fail(RMPC_EINVAL, "LTV needs uref_rows >= N (%d < %d)", uref_rows, N);
     }
     if (ref_rows < 1 || uref_rows < 1) return fail(RMPC_EINVAL, "empty reference arrays");
-    if (!p->soft && n_obs > 0)
-        return fail(RMPC_ENOTSUP, "use_soft_constraints=False with obstacles (hard half-spaces) is not supported yet");
     if (p->precision != RMPC_F64 && p->precision != RMPC_F32)
         return fail(RMPC_EINVAL, "precision %d is neither RMPC_F64 nor RMPC_F32", p->precision);
     if (!(p->dt > 0) || !(p->slack_penalty >= 0) || !(p->R[0] > 0) || !(p->R[1] > 0))
@@ -274,7 +272,9 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
     HIP_TRY(ensure_ws(c, L, B));
     const MpcDevParams d = to_dev(p);
     const bool f32 = p->precision == RMPC_F32;
-    const bool fast = p->formulation == RMPC_LTV && rmpc_mpc_fast_supported(p->horizon, bs, p->precision) &&
+    // hard half-spaces (soft = 0 with obstacles): augmented-Lagrangian rounds in the generic kernel
+    const bool hard = !p->soft && n_obs > 0;
+    const bool fast = p->formulation == RMPC_LTV && !hard && rmpc_mpc_fast_supported(p->horizon, bs, p->precision) &&
                       !getenv("RMPC_DISABLE_FAST");
     if (!fast && f32)                      // fp32 arithmetic: the generic kernel on a float record
         HIP_TRY(rmpc_launch_mpc_f32(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,

@@ -21,6 +21,7 @@ struct MpcLayout {
     int A0, A1, B0, B1, US0, US1, XS0, XS1, XS2;
     int LO0, LO1, HI0, HI1, BF0, BF1;
     int HN0, HN1, HB, HACT;
+    int HBO;   // original hinge right-hand sides (HB = HBO + shift in the hard-constraint mode)
     int K;     // 8 * nb: K rows (6) + k (2), per block
     int X0, X1, X2, U0, U1, Z0, Z1, G0, G1;
     int REC;

@@ -79,7 +79,7 @@ __device__ void setup_ltv(const MpcArgs<T> &a, const WaveTile<T> &w, int64_t b, 
                 const double ddx = px - ox, ddy = py - oy;
                 const double dist = sqrt(ddx * ddx + ddy * ddy);
                 const int idx = k * L.no + o;
-                if (p.soft && dist > 0.01) {
+                if (dist > 0.01) {                     // soft (slack) or hard row alike
                     const double nx = ddx / dist, ny = ddy / dist;
                     const double safe = p.d_safe + a.obstacles[3 * o + 2];
                     w(L.HN0 + idx) = (T)nx;
@@ -90,6 +90,7 @@ __device__ void setup_ltv(const MpcArgs<T> &a, const WaveTile<T> &w, int64_t b, 
                     w(L.HN1 + idx) = (T)0;
                     w(L.HB + idx) = (T)-1e30;
                 }
+                w(L.HBO + idx) = w(L.HB + idx);
                 w(L.HACT + idx) = (T)0;
             }
         }
@@ -160,7 +161,7 @@ __device__ void setup_lti(const MpcArgs<T> &a, const WaveTile<T> &w, int64_t b, 
                 const double ddx = px - ox, ddy = py - oy;
                 const double dist = sqrt(ddx * ddx + ddy * ddy);
                 const int idx = k * L.no + o;
-                if (p.soft && dist > 0.01) {
+                if (dist > 0.01) {
                     const double nx = ddx / dist, ny = ddy / dist;
                     w(L.HN0 + idx) = (T)nx;
                     w(L.HN1 + idx) = (T)ny;
@@ -170,6 +171,7 @@ __device__ void setup_lti(const MpcArgs<T> &a, const WaveTile<T> &w, int64_t b, 
                     w(L.HN1 + idx) = (T)0;
                     w(L.HB + idx) = (T)-1e30;
                 }
+                w(L.HBO + idx) = w(L.HB + idx);
                 w(L.HACT + idx) = (T)0;
             }
         }
@@ -381,6 +383,120 @@ __device__ uint64_t set_signature(const MpcLayout &L, const WaveTile<T> &w) {
     return h;
 }
 
+// One solve of the (soft, or shifted-hard) piecewise-quadratic problem for the robot's
+// current record: PDAS from the stored active sets, then projected Newton + Armijo.
+// `it` counts Riccati solves; stops at `max_iter`.  Returns 1 if certified (exact KKT).
+template <typename T>
+__device__ int solve_inner(const MpcDevParams &p, const MpcLayout &L, const WaveTile<T> &w,
+                           const T x0[3], int &it, const int max_iter) {
+    int cert = 0;
+    const int it0 = it;
+    // ---- phase 1: primal-dual active set (capped; a repeated signature = cycling)
+    uint64_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    for (; it < max_iter && it - it0 < RMPC_PDAS_ITERS;) {
+        it++;
+        if (!riccati_pass(p, L, w, x0, 0)) { cert = 1; break; }
+        const uint64_t sig = set_signature(L, w);
+        if (sig == h0 || sig == h1 || sig == h2 || sig == h3) break;
+        h3 = h2; h2 = h1; h1 = h0; h0 = sig;
+    }
+    if (!cert && it < max_iter) {
+        // ---- phase 2: projected Newton + Armijo from the projected last iterate
+        for (int j = 0; j < L.nb; j++) {
+            w(L.Z0 + j) = clampv(w(L.U0 + j), w(L.LO0 + j), w(L.HI0 + j));
+            w(L.Z1 + j) = clampv(w(L.U1 + j), w(L.LO1 + j), w(L.HI1 + j));
+        }
+        T F = simulate_F(p, L, w, x0, (T)-1, (T *)nullptr, 0);
+        int stalled = 0;
+        while (it < max_iter) {
+            gradient(p, L, w);
+            T wmax = 0;
+            for (int j = 0; j < L.nb; j++) {
+                const T z0 = w(L.Z0 + j), z1 = w(L.Z1 + j);
+                wmax = fmax(wmax, fabs(z0 - clampv(z0 - w(L.G0 + j), w(L.LO0 + j), w(L.HI0 + j))));
+                wmax = fmax(wmax, fabs(z1 - clampv(z1 - w(L.G1 + j), w(L.LO1 + j), w(L.HI1 + j))));
+            }
+            const T eps = fmin(SetTol<T>::pn, wmax);
+            for (int k = 1; k < L.N; k++)
+                for (int o = 0; o < L.no; o++) {
+                    const int idx = k * L.no + o;
+                    const T r = w(L.HB + idx) - w(L.HN0 + idx) * w(L.X0 + k) - w(L.HN1 + idx) * w(L.X1 + k);
+                    w(L.HACT + idx) = r > (T)0 ? (T)1 : (T)0;
+                }
+            for (int j = 0; j < L.nb; j++) {
+                const T z0 = w(L.Z0 + j), z1 = w(L.Z1 + j), g0 = w(L.G0 + j), g1 = w(L.G1 + j);
+                w(L.BF0 + j) = (z0 <= w(L.LO0 + j) + eps && g0 > 0) ? (T)1
+                               : ((z0 >= w(L.HI0 + j) - eps && g0 < 0) ? (T)2 : (T)0);
+                w(L.BF1 + j) = (z1 <= w(L.LO1 + j) + eps && g1 > 0) ? (T)1
+                               : ((z1 >= w(L.HI1 + j) - eps && g1 < 0) ? (T)2 : (T)0);
+            }
+            it++;
+            if (!riccati_pass(p, L, w, x0, 1)) { cert = 1; break; }
+            T alpha = 1, Ft = F, gd = 0;
+            int acc = 0;
+            for (int ls = 0; ls < 40; ls++) {
+                Ft = simulate_F(p, L, w, x0, alpha, &gd, 0);
+                if (Ft <= F + (T)1e-4 * gd) { acc = 1; break; }
+                alpha *= (T)0.5;
+            }
+            if (!acc) { stalled = 1; break; }
+            simulate_F(p, L, w, x0, alpha, &gd, 1);   // commit Z, X
+            F = Ft;
+        }
+        if (!cert) {
+            // best box-feasible point: Z (re-simulate so X matches)
+            simulate_F(p, L, w, x0, (T)-1, (T *)nullptr, 0);
+            for (int j = 0; j < L.nb; j++) { w(L.U0 + j) = w(L.Z0 + j); w(L.U1 + j) = w(L.Z1 + j); }
+        }
+        (void)stalled;
+    }
+    return cert;
+}
+
+// Hard half-spaces (use_soft_constraints=False, mpc_controller.py:383-386 / :197-200 with the
+// rows of :439-468 / :238-270 as plain inequalities): augmented Lagrangian over the same
+// solver.  Each outer round solves the soft problem with penalty rho_h and the rows shifted
+// by s_i >= 0 (HB = HBO + s), then s_i <- max(0, r_i + s_i).  A fixed point is exactly the
+// KKT point of the hard QP (multipliers 2 rho_h s_i); rows at k = 0 act on the fixed dx_0
+// and, when violated, make the QP infeasible -- the reference's solver then reports
+// infeasibility and the fallback law applies (:521-522), as it does here when the shifts
+// do not converge.
+template <typename T> struct HardAlm;
+template <> struct HardAlm<double> {
+    static constexpr double rho = 1e6, tol = 1e-12, k0_tol = 1e-9;
+    static constexpr int outer = 60;
+};
+template <> struct HardAlm<float> {
+    static constexpr float rho = 1e3f, tol = 1e-5f, k0_tol = 1e-5f;
+    static constexpr int outer = 60;
+};
+
+template <typename T>
+__device__ int solve_hard(const MpcDevParams &p, const MpcLayout &L, const WaveTile<T> &w,
+                          const T x0[3], int &it, const int max_iter) {
+    for (int o = 0; o < L.no; o++)        // k = 0 rows: fixed state, feasibility is decided
+        if (w(L.HB + o) - w(L.HN0 + o) * x0[0] - w(L.HN1 + o) * x0[1] > HardAlm<T>::k0_tol) return 0;
+    MpcDevParams ph = p;
+    ph.rho = HardAlm<T>::rho;
+    for (int round = 0; round < HardAlm<T>::outer; round++) {
+        if (!solve_inner(ph, L, w, x0, it, it + max_iter)) return 0;
+        T viol = 0;
+        for (int k = 1; k < L.N; k++)
+            for (int o = 0; o < L.no; o++) {
+                const int idx = k * L.no + o;
+                const T hbo = w(L.HBO + idx);
+                if (hbo < (T)-1e29) continue;                   // row absent (dist <= 0.01)
+                const T sh = w(L.HB + idx) - hbo;
+                const T rs = w(L.HB + idx) - w(L.HN0 + idx) * w(L.X0 + k) - w(L.HN1 + idx) * w(L.X1 + k);
+                const T ns = rs > (T)0 ? rs : (T)0;
+                viol = fmax(viol, fabs(ns - sh));
+                w(L.HB + idx) = hbo + ns;
+            }
+        if (viol <= HardAlm<T>::tol) return 1;
+    }
+    return 0;
+}
+
 // USE_LDS: the whole robot record lives in LDS (workgroup = blockDim lanes, sized by the
 // host so the records fit in 160 KiB) -- used for the small retry lists, where latency
 // per robot, not occupancy, decides the launch time.
@@ -408,65 +524,9 @@ __global__ __launch_bounds__(256) void mpc_solve_kernel(MpcArgs<T> a) {
     int cert = 0, it = 0;
     const int max_iter = p.max_iter;
     if (finite) {
-        // ---- phase 1: primal-dual active set (capped; a repeated signature = cycling)
-        uint64_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-        for (; it < max_iter && it < RMPC_PDAS_ITERS;) {
-            it++;
-            if (!riccati_pass(p, L, w, x0, 0)) { cert = 1; break; }
-            const uint64_t sig = set_signature(L, w);
-            if (sig == h0 || sig == h1 || sig == h2 || sig == h3) break;
-            h3 = h2; h2 = h1; h1 = h0; h0 = sig;
-        }
-        if (!cert && it < max_iter) {
-            // ---- phase 2: projected Newton + Armijo from the projected last iterate
-            for (int j = 0; j < L.nb; j++) {
-                w(L.Z0 + j) = clampv(w(L.U0 + j), w(L.LO0 + j), w(L.HI0 + j));
-                w(L.Z1 + j) = clampv(w(L.U1 + j), w(L.LO1 + j), w(L.HI1 + j));
-            }
-            T F = simulate_F(p, L, w, x0, (T)-1, (T *)nullptr, 0);
-            int stalled = 0;
-            while (it < max_iter) {
-                gradient(p, L, w);
-                T wmax = 0;
-                for (int j = 0; j < L.nb; j++) {
-                    const T z0 = w(L.Z0 + j), z1 = w(L.Z1 + j);
-                    wmax = fmax(wmax, fabs(z0 - clampv(z0 - w(L.G0 + j), w(L.LO0 + j), w(L.HI0 + j))));
-                    wmax = fmax(wmax, fabs(z1 - clampv(z1 - w(L.G1 + j), w(L.LO1 + j), w(L.HI1 + j))));
-                }
-                const T eps = fmin(SetTol<T>::pn, wmax);
-                for (int k = 1; k < L.N; k++)
-                    for (int o = 0; o < L.no; o++) {
-                        const int idx = k * L.no + o;
-                        const T r = w(L.HB + idx) - w(L.HN0 + idx) * w(L.X0 + k) - w(L.HN1 + idx) * w(L.X1 + k);
-                        w(L.HACT + idx) = r > (T)0 ? (T)1 : (T)0;
-                    }
-                for (int j = 0; j < L.nb; j++) {
-                    const T z0 = w(L.Z0 + j), z1 = w(L.Z1 + j), g0 = w(L.G0 + j), g1 = w(L.G1 + j);
-                    w(L.BF0 + j) = (z0 <= w(L.LO0 + j) + eps && g0 > 0) ? (T)1
-                                   : ((z0 >= w(L.HI0 + j) - eps && g0 < 0) ? (T)2 : (T)0);
-                    w(L.BF1 + j) = (z1 <= w(L.LO1 + j) + eps && g1 > 0) ? (T)1
-                                   : ((z1 >= w(L.HI1 + j) - eps && g1 < 0) ? (T)2 : (T)0);
-                }
-                it++;
-                if (!riccati_pass(p, L, w, x0, 1)) { cert = 1; break; }
-                T alpha = 1, Ft = F, gd = 0;
-                int acc = 0;
-                for (int ls = 0; ls < 40; ls++) {
-                    Ft = simulate_F(p, L, w, x0, alpha, &gd, 0);
-                    if (Ft <= F + (T)1e-4 * gd) { acc = 1; break; }
-                    alpha *= (T)0.5;
-                }
-                if (!acc) { stalled = 1; break; }
-                simulate_F(p, L, w, x0, alpha, &gd, 1);   // commit Z, X
-                F = Ft;
-            }
-            if (!cert) {
-                // best box-feasible point: Z (re-simulate so X matches)
-                simulate_F(p, L, w, x0, (T)-1, (T *)nullptr, 0);
-                for (int j = 0; j < L.nb; j++) { w(L.U0 + j) = w(L.Z0 + j); w(L.U1 + j) = w(L.Z1 + j); }
-            }
-            (void)stalled;
-        }
+        if (!p.soft && L.no > 0) cert = solve_hard(p, L, w, x0, it, max_iter);
+        else cert = solve_inner(p, L, w, x0, it, max_iter);
+        if (!p.soft && L.no > 0 && !cert) finite = 0;        // infeasible / unconverged -> fallback
     }
     // ---- outputs
     const int N = L.N;
@@ -490,7 +550,7 @@ __global__ __launch_bounds__(256) void mpc_solve_kernel(MpcArgs<T> a) {
                     const int idx = k * L.no + o;
                     const double r = (double)(w(L.HB + idx) - w(L.HN0 + idx) * w(L.X0 + k) -
                                               w(L.HN1 + idx) * w(L.X1 + k));
-                    if (r > 0) {
+                    if (r > 0 && p.soft) {                  // hard rows carry no slack term
                         J += p.rho * r * r;
                         if (r > 1e-6) used = 1;             // :485 slack.value > 1e-6
                     }
@@ -577,6 +637,7 @@ MpcLayout rmpc_mpc_layout(int N, int bs, int no) {
     L.LO0 = take(L.nb); L.LO1 = take(L.nb); L.HI0 = take(L.nb); L.HI1 = take(L.nb);
     L.BF0 = take(L.nb); L.BF1 = take(L.nb);
     L.HN0 = take(N * no); L.HN1 = take(N * no); L.HB = take(N * no); L.HACT = take(N * no);
+    L.HBO = take(N * no);
     L.K = take(8 * L.nb);
     L.X0 = take(N + 1); L.X1 = take(N + 1); L.X2 = take(N + 1);
     L.U0 = take(L.nb); L.U1 = take(L.nb);

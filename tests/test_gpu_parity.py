@@ -154,6 +154,52 @@ def test_mpc_kernel_matches_exact_qp_oracle(rm, N, bs, scen, ltv, noise, seed, B
         assert np.all(sc == 5)
 
 
+HARD_CASES = [  # (N, bs, scenario, ltv, noise, seed, B): use_soft_constraints=False
+    (20, 1, "default", True, (0.05, 0.05, 0.1), 7, 40),
+    (20, 1, "default", True, (0.3, 0.3, 0.5), 7, 40),
+    (10, 1, "dense", True, (0.2, 0.2, 0.3), 7, 40),
+    (6, 2, "corridor", True, (0.2, 0.2, 0.3), 8, 40),
+    (20, 1, "default", False, (0.2, 0.2, 0.3), 7, 40),    # LTI solve()
+]
+
+
+@pytest.mark.parametrize("N,bs,scen,ltv,noise,seed,B", HARD_CASES)
+def test_mpc_hard_constraints_match_oracle(rm, N, bs, scen, ltv, noise, seed, B):
+    """use_soft_constraints=False (mpc_controller.py:383-386, :465-468): hard half-spaces.
+    Feasible robots: |du|, |dx| <= 1e-9 against the exact QP oracle, no slack, cost without
+    a slack term.  Infeasible robots (a violated k = 0 row on the fixed initial state): the
+    fallback law on both sides (:521-522), step count unchanged."""
+    obs = ompc.scenario_obstacles(scen)
+    x0, xr, ur = _workload(N, B, seed, noise)
+    p = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                              0.02, block_size=bs, ltv=ltv, soft=False)
+    sc = np.full(B, 4, np.int32)
+    out = rm.batch.mpc_solve_batch(p, x0, xr, ur, obs, step_count=sc if ltv else None)
+    oc = ompc.MPCController(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                            0.02, "OSQP", bs)
+    n_opt = 0
+    for b in range(B):
+        oc._step_count = 4
+        s = (oc.solve_with_ltv(x0[b], xr[b], ur[b], obs, use_soft_constraints=False) if ltv
+             else oc.solve(x0[b], xr[b], ur[b], obs, use_soft_constraints=False))
+        if s.status == "optimal":
+            n_opt += 1
+            assert out["status"][b] == 0, b
+            np.testing.assert_allclose(out["u_seq"][b], s.control_sequence, atol=1e-9, rtol=0)
+            np.testing.assert_allclose(out["x_pred"][b], s.predicted_states, atol=1e-9, rtol=0)
+            assert abs(out["cost"][b] - s.cost) <= 1e-9 * max(1.0, abs(s.cost))
+            assert not out["slack_used"][b]
+            if ltv:
+                assert sc[b] == 5
+        else:
+            assert out["status"][b] == 2, b
+            np.testing.assert_allclose(out["u0"][b], s.optimal_control, atol=1e-12, rtol=0)
+            assert np.isinf(out["cost"][b])
+            if ltv:
+                assert sc[b] == 4
+    assert n_opt >= B // 2
+
+
 def test_mpc_full_config3_vs_cpu_port(rm):
     """BASELINE config 3 at full size (B=65536, N=20, 3 obstacles): every robot against the
     C restatement; run twice to check determinism."""

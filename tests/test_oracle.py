@@ -168,3 +168,43 @@ def test_fallback_law():
                                [np.clip(1 - 0.5, -2, 2), np.clip(1 - 0.5 * e2, -3, 3)])
     assert s.status == "fallback" and s.cost == float("inf")
     assert s.control_sequence.shape == (6, 2) and s.predicted_states.shape == (7, 3)
+
+
+def test_hard_constraint_oracle_properties():
+    """use_soft_constraints=False (mpc_controller.py:383-386): every kept obstacle row holds
+    at the oracle's optimum (no slack), the hard optimum costs at least the soft one, and a
+    violated k = 0 row (fixed initial state) makes the QP infeasible -> fallback law.
+    Parity unpinned by reference artefacts (no logged run uses hard constraints)."""
+    rng = np.random.default_rng(7)
+    N = 10
+    obs = mpc.default_obstacles()
+    t0 = rng.uniform(0, 4 * np.pi, 12)
+    xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, t0, N + 1)
+    x0 = xr[:, 0] + rng.normal(0, (0.3, 0.3, 0.5), (12, 3))
+    oc = mpc.MPCController(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+    seen = set()
+    for b in range(12):
+        k0_viol = False
+        for (ox, oy, r) in obs:
+            d = np.hypot(xr[b, 0, 0] - ox, xr[b, 0, 1] - oy)
+            if d > 0.01:
+                n = (xr[b, 0, :2] - (ox, oy)) / d
+                k0_viol |= bool(n @ (x0[b, :2] - (ox, oy)) < 0.3 + r)
+        hard = oc.solve_with_ltv(x0[b], xr[b], ur[b], obs, use_soft_constraints=False)
+        seen.add(hard.status)
+        if k0_viol:
+            assert hard.status == "fallback"
+            continue
+        soft = oc.solve_with_ltv(x0[b], xr[b], ur[b], obs)
+        if hard.status != "optimal":
+            continue
+        assert not hard.slack_used
+        assert hard.cost >= soft.cost - 1e-9
+        for (ox, oy, r) in obs:
+            for k in range(N):
+                p = xr[b, k, :2]
+                d = np.hypot(*(p - (ox, oy)))
+                if d > 0.01:
+                    n = (p - (ox, oy)) / d
+                    assert n @ (hard.predicted_states[k, :2] - (ox, oy)) >= 0.3 + r - 1e-9
+    assert seen == {"optimal", "fallback"}
