@@ -78,7 +78,7 @@ struct RmpcCtx {
     DevBuf fast_gains, fast_usol, retry, retry2, retry_count, prof, retry_sets;
     // closed-loop rollout state (rmpc_rollout_batch)
     DevBuf ro_x, ro_xr, ro_ur, ro_u, ro_step, ro_cache, ro_prev, ro_since, ro_status, ro_used,
-        ro_risk, ro_counts;
+        ro_risk, ro_counts, ro_off;
     // stage timing of the last MPC launch (rmpc_ctx_set_timing): events before/after
     // the lane-per-robot, wave-per-robot and generic stages
     bool timing = false;
@@ -136,7 +136,7 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     c->retry2.release();
     c->retry_sets.release();
     for (DevBuf *d : {&c->ro_x, &c->ro_xr, &c->ro_ur, &c->ro_u, &c->ro_step, &c->ro_cache, &c->ro_prev,
-                      &c->ro_since, &c->ro_status, &c->ro_used, &c->ro_risk, &c->ro_counts})
+                      &c->ro_since, &c->ro_status, &c->ro_used, &c->ro_risk, &c->ro_counts, &c->ro_off})
         d->release();
     c->prof.release();
     c->retry_count.release();
@@ -211,6 +211,7 @@ static MpcDevParams to_dev(const RmpcMpcParams *p) {
     d.soft = p->soft;
     d.max_iter = p->max_iter > 0 ? p->max_iter : 64;
     d.ramp_up_steps = p->ramp_up_steps > 0 ? p->ramp_up_steps : 10;
+    d.ref_off = nullptr;
     return d;
 }
 
@@ -224,6 +225,7 @@ static LqrDevParams to_dev(const RmpcLqrParams *p) {
     d.omega_max = p->omega_max;
     d.max_iter = p->max_iter > 0 ? p->max_iter : 64;
     d.use_cache = p->use_cache;
+    d.ref_off = nullptr;
     return d;
 }
 
@@ -266,11 +268,13 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                       const double *x_refs, int32_t ref_rows, const double *u_refs, int32_t uref_rows,
                       const double *obstacles, int32_t n_obs, int32_t *step_count, double *u0,
                       double *u_seq, double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
-                      int32_t *iters, const int32_t *index, const int32_t *count, hipStream_t s) {
+                      int32_t *iters, const int32_t *index, const int32_t *count, hipStream_t s,
+                      const int32_t *ref_off = nullptr) {
     const int bs = p->formulation == RMPC_LTV ? p->block_size : 1;
     const MpcLayout L = rmpc_mpc_layout(p->horizon, bs, n_obs);
     HIP_TRY(ensure_ws(c, L, B));
-    const MpcDevParams d = to_dev(p);
+    MpcDevParams d = to_dev(p);
+    d.ref_off = ref_off;
     const bool f32 = p->precision == RMPC_F32;
     // hard half-spaces (soft = 0 with obstacles): augmented-Lagrangian rounds in the generic kernel
     const bool hard = !p->soft && n_obs > 0;
@@ -311,6 +315,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         // default cap (sweeps with the lane-group tail): 7 at N <= 20 (BASELINE config 3), 12
         // beyond (config 4)
         a.pdas_cap = getenv("RMPC_FAST_CAP") ? atoi(getenv("RMPC_FAST_CAP")) : (p->horizon <= 20 ? 7 : 12);
+        a.screen = !getenv("RMPC_NO_SCREEN");
         const bool warm = !getenv("RMPC_COLD_TAIL");
         if (warm) {
             HIP_TRY(c->retry_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
@@ -625,13 +630,12 @@ extern "C" int rmpc_risk_batch(RmpcCtx *c, const RmpcRiskParams *rp, int64_t B, 
     return RMPC_OK;
 }
 
-extern "C" int rmpc_hybrid_step_batch_dev(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams *lp,
-                                          const RmpcMpcParams *mp, int64_t B, const double *x,
-                                          const double *x_refs, int32_t ref_rows, const double *u_refs,
-                                          int32_t uref_rows, const double *obstacles, int32_t n_obs,
-                                          int32_t *prev_ctrl, int32_t *steps_since, int32_t *step_count,
-                                          RmpcLqrCache *cache, double *u_out, uint8_t *used_mpc,
-                                          double *risk_out, void *stream) {
+static int hybrid_step(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams *lp,
+                       const RmpcMpcParams *mp, int64_t B, const double *x, const double *x_refs,
+                       int32_t ref_rows, const double *u_refs, int32_t uref_rows, const double *obstacles,
+                       int32_t n_obs, int32_t *prev_ctrl, int32_t *steps_since, int32_t *step_count,
+                       RmpcLqrCache *cache, double *u_out, uint8_t *used_mpc, double *risk_out, void *stream,
+                       const int32_t *ref_off) {
     if (!c || !rp || !lp) return fail(RMPC_EINVAL, "ctx/params is NULL");
     RC(check_mpc_params(mp, ref_rows, uref_rows, n_obs));
     RC(check_lqr(lp));
@@ -651,13 +655,26 @@ extern "C" int rmpc_hybrid_step_batch_dev(RmpcCtx *c, const RmpcRiskParams *rp, 
     HIP_TRY(rmpc_launch_hybrid_decide(to_dev(rp), B, x, obstacles, n_obs, prev_ctrl, steps_since, used_mpc,
                                       risk_out, (int32_t *)c->idx_lqr.p, (int32_t *)c->idx_mpc.p, cnt, s));
     // LQR branch: x_ref / u_ref = row 0 of the segment (get_reference_at_index(k))
-    HIP_TRY(rmpc_launch_lqr_control(to_dev(lp), B, x, x_refs, ref_rows * 3, u_refs, uref_rows * 2, cache,
+    LqrDevParams ld = to_dev(lp);
+    ld.ref_off = ref_off;
+    HIP_TRY(rmpc_launch_lqr_control(ld, B, x, x_refs, ref_rows * 3, u_refs, uref_rows * 2, cache,
                                     u_out, nullptr, nullptr, nullptr, nullptr, (const int32_t *)c->idx_lqr.p,
                                     cnt, s));
     // MPC branch: solve_with_ltv on the segment; writes u0 straight into u_out
     return launch_mpc(c, mp, B, x, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs, step_count, u_out,
                       nullptr, nullptr, nullptr, (int32_t *)c->hyb_status.p, nullptr, nullptr,
-                      (const int32_t *)c->idx_mpc.p, cnt + 1, s);
+                      (const int32_t *)c->idx_mpc.p, cnt + 1, s, ref_off);
+}
+
+extern "C" int rmpc_hybrid_step_batch_dev(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams *lp,
+                                          const RmpcMpcParams *mp, int64_t B, const double *x,
+                                          const double *x_refs, int32_t ref_rows, const double *u_refs,
+                                          int32_t uref_rows, const double *obstacles, int32_t n_obs,
+                                          int32_t *prev_ctrl, int32_t *steps_since, int32_t *step_count,
+                                          RmpcLqrCache *cache, double *u_out, uint8_t *used_mpc,
+                                          double *risk_out, void *stream) {
+    return hybrid_step(c, rp, lp, mp, B, x, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs, prev_ctrl,
+                       steps_since, step_count, cache, u_out, used_mpc, risk_out, stream, nullptr);
 }
 
 extern "C" int rmpc_hybrid_step_batch(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams *lp,
@@ -767,8 +784,16 @@ extern "C" int rmpc_rollout_batch_dev(RmpcCtx *c, const RmpcRolloutParams *rp, c
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = pick(c, stream);
     HIP_TRY(c->ro_x.ensure((size_t)B * 3 * sizeof(double)));
-    HIP_TRY(c->ro_xr.ensure((size_t)B * rows * 3 * sizeof(double)));
-    HIP_TRY(c->ro_ur.ensure((size_t)B * rows * 2 * sizeof(double)));
+    // references: the generate() table, built once with `rows` copies of its last row appended,
+    // so robot b's segment at step k is the `rows` rows from min(start_b + k, len - 1) on
+    // (get_trajectory_segment's end clamp, reference_generator.py:299-326) -- the solves read
+    // them from this shared table through per-robot row offsets (RMPC_ROLLOUT_REFS=copy: the
+    // per-step per-robot segment copies instead)
+    const bool copy_refs = getenv("RMPC_ROLLOUT_REFS") && !strcmp(getenv("RMPC_ROLLOUT_REFS"), "copy");
+    const int64_t tab_rows = (int64_t)rp->table_len + rows;
+    HIP_TRY(c->ro_xr.ensure((size_t)(copy_refs ? B * rows : tab_rows) * 3 * sizeof(double)));
+    HIP_TRY(c->ro_ur.ensure((size_t)(copy_refs ? B * rows : tab_rows) * 2 * sizeof(double)));
+    HIP_TRY(c->ro_off.ensure((size_t)B * sizeof(int32_t)));
     HIP_TRY(c->ro_u.ensure((size_t)B * 2 * sizeof(double)));
     HIP_TRY(c->ro_step.ensure((size_t)B * sizeof(int32_t)));
     HIP_TRY(c->ro_cache.ensure((size_t)B * sizeof(RmpcLqrCache)));
@@ -788,21 +813,30 @@ extern "C" int rmpc_rollout_batch_dev(RmpcCtx *c, const RmpcRolloutParams *rp, c
     HIP_TRY(hipMemsetAsync(counts, 0, 4 * sizeof(unsigned long long), s));
     HIP_TRY(rmpc_launch_rollout_init(B, start_index, x0, rp->table_len, rp->A, rp->a, rp->dt, x, prev, since,
                                      step, cache, states, rp->steps, s));
+    int32_t *off = copy_refs ? nullptr : (int32_t *)c->ro_off.p;
+    if (!copy_refs)          // one "robot" whose segment is the whole padded table
+        HIP_TRY(rmpc_launch_figure8_table(1, nullptr, 0, (int)tab_rows, rp->table_len, rp->A, rp->a, rp->dt, xr,
+                                          ur, s));
+    LqrDevParams ld = lp ? to_dev(lp) : LqrDevParams{};
+    ld.ref_off = off;
     for (int k = 0; k < rp->steps; k++) {
-        HIP_TRY(rmpc_launch_figure8_table(B, start_index, k, rows, rp->table_len, rp->A, rp->a, rp->dt, xr, ur,
-                                          s));
+        if (copy_refs)
+            HIP_TRY(rmpc_launch_figure8_table(B, start_index, k, rows, rp->table_len, rp->A, rp->a, rp->dt, xr,
+                                              ur, s));
+        else
+            HIP_TRY(rmpc_launch_ref_offsets(B, start_index, k, rp->table_len - 1, off, s));
         if (mode == 0) {                                   // run_simulation.py:77-80
-            HIP_TRY(rmpc_launch_lqr_control(to_dev(lp), B, x, xr, 3, ur, 2, cache, u, nullptr, nullptr, nullptr,
+            HIP_TRY(rmpc_launch_lqr_control(ld, B, x, xr, 3, ur, 2, cache, u, nullptr, nullptr, nullptr,
                                             nullptr, nullptr, nullptr, s));
         } else if (mode == 1) {                            // :250-259, zero-order hold in u
             if (k % rp->mpc_rate == 0) {
                 RC(launch_mpc(c, mp, B, x, xr, rows, ur, rows, obstacles, n_obs, step, u, nullptr, nullptr,
-                              nullptr, status, nullptr, nullptr, nullptr, nullptr, s));
+                              nullptr, status, nullptr, nullptr, nullptr, nullptr, s, off));
                 HIP_TRY(rmpc_launch_status_count(B, status, nullptr, counts, s));
             }
         } else {                                           // :525-559
-            RC(rmpc_hybrid_step_batch_dev(c, kp, lp, mp, B, x, xr, rows, ur, rows, obstacles, n_obs, prev,
-                                          since, step, cache, u, used_now, (double *)c->ro_risk.p, s));
+            RC(hybrid_step(c, kp, lp, mp, B, x, xr, rows, ur, rows, obstacles, n_obs, prev, since, step, cache, u,
+                           used_now, (double *)c->ro_risk.p, s, off));
             HIP_TRY(rmpc_launch_status_count(B, (const int32_t *)c->hyb_status.p, used_now, counts, s));
         }
         HIP_TRY(rmpc_launch_rollout_plant(B, x, u, rp->dt, rp->v_max, rp->omega_max, rp->plant_method, k,

@@ -13,7 +13,15 @@ struct MpcDevParams {
     double Q[3], R[2], P[3];
     double d_safe, rho, v_max, omega_max, dt;
     int ltv, soft, max_iter, ramp_up_steps;
+    // optional per-robot first reference row (rollouts: rows of one shared, end-padded Figure-8
+    // table); NULL = robot b's segment starts at row b * ref_rows of its own arrays
+    const int32_t *ref_off;
 };
+
+// first row of robot b's reference segment (x_refs / u_refs are [rows][3] / [rows][2])
+__host__ __device__ __forceinline__ size_t ref_row0(const int32_t *ref_off, int64_t b, int rows) {
+    return ref_off ? (size_t)ref_off[b] : (size_t)b * (size_t)rows;
+}
 
 // Offsets (in elements) of the fields of one robot's workspace record.
 struct MpcLayout {
@@ -44,6 +52,7 @@ struct MpcFastArgs {
     const int32_t *index, *count;    // optional robot index list (device-side length)
     int32_t *retry, *retry_count;    // robots handed to the next stage
     int pdas_cap;                    // PDAS solves before a robot is handed on
+    int screen;                      // forward-sweep row screening on (RMPC_NO_SCREEN=1: off)
     unsigned long long *prof;        // diagnostics: per-phase cycle counters (may be null)
     uint32_t *retry_sets;            // per retry slot: hinge flags [N], box states [NB], iters
                                      // (warm start of the next stage; may be null)
@@ -92,6 +101,7 @@ struct LqrDevParams {
     double Q[3], R[2];
     double dt, v_max, omega_max;
     int max_iter, use_cache;
+    const int32_t *ref_off;    // as MpcDevParams::ref_off (NULL: strided per-robot rows)
 };
 
 hipError_t rmpc_launch_lqr_control(const LqrDevParams &p, int64_t B, const double *x,
@@ -121,6 +131,8 @@ hipError_t rmpc_launch_plant(int64_t B, const double *x, const double *u, double
 hipError_t rmpc_launch_figure8_table(int64_t B, const int32_t *start, int32_t k, int rows, int32_t table_len,
                                      double A, double a, double dt, double *x_refs, double *u_refs,
                                      hipStream_t stream);
+hipError_t rmpc_launch_ref_offsets(int64_t B, const int32_t *start, int32_t k, int32_t last, int32_t *off,
+                                   hipStream_t stream);
 hipError_t rmpc_launch_rollout_init(int64_t B, const int32_t *start, const double *x0, int32_t table_len,
                                     double A, double a, double dt, double *x, int32_t *prev_ctrl,
                                     int32_t *since, int32_t *step_count, RmpcLqrCache *cache, double *states,

@@ -146,8 +146,8 @@ __global__ __launch_bounds__(256) void lqr_control_kernel(LqrDevParams p, int64_
     if (t >= n) return;
     const int64_t b = index ? (int64_t)index[t] : t;
     const double *xb = x + 3 * b;
-    const double *xr = x_ref + (size_t)xref_stride * b;
-    const double *ur = u_ref + (size_t)uref_stride * b;
+    const double *xr = x_ref + (p.ref_off ? (size_t)p.ref_off[b] * 3 : (size_t)xref_stride * b);
+    const double *ur = u_ref + (p.ref_off ? (size_t)p.ref_off[b] * 2 : (size_t)uref_stride * b);
     const double v = ur[0], th = xr[2];
     double K[6];
     int st = RMPC_OPTIMAL;

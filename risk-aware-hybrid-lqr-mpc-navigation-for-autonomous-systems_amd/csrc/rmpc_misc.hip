@@ -187,6 +187,15 @@ __global__ __launch_bounds__(256) void figure8_table_kernel(int64_t B, const int
     fig8_point(A, a, dt, (double)j * dt, xr + 3 * g, ur + 2 * g);
 }
 
+// per-robot first reference row of rollout step k in the end-padded table
+__global__ __launch_bounds__(256) void ref_offsets_kernel(int64_t B, const int32_t *start, int32_t k, int32_t last,
+                                                          int32_t *off) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int64_t j = (int64_t)(start ? start[b] : 0) + k;
+    off[b] = (int32_t)(j < last ? j : last);
+}
+
 // rollout start: x = x0[b] or the reference at the start row; clear per-robot state
 __global__ __launch_bounds__(256) void rollout_init_kernel(int64_t B, const int32_t *start, const double *x0,
                                                            int32_t table_len, double A, double a, double dt,
@@ -284,6 +293,13 @@ hipError_t rmpc_launch_figure8_table(int64_t B, const int32_t *start, int32_t k,
     if (B <= 0) return hipSuccess;
     hipLaunchKernelGGL(figure8_table_kernel, dim3(nblk(B * rows, 256)), dim3(256), 0, stream, B, start, k, rows,
                        table_len, A, a, dt, x_refs, u_refs);
+    return hipGetLastError();
+}
+
+hipError_t rmpc_launch_ref_offsets(int64_t B, const int32_t *start, int32_t k, int32_t last, int32_t *off,
+                                   hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ref_offsets_kernel, dim3(nblk(B, 256)), dim3(256), 0, stream, B, start, k, last, off);
     return hipGetLastError();
 }
 

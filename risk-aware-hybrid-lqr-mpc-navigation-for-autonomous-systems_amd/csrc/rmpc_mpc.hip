@@ -46,8 +46,8 @@ __device__ void setup_ltv(const MpcArgs<T> &a, const WaveTile<T> &w, int64_t b, 
     const MpcLayout &L = a.L;
     const MpcDevParams &p = a.prm;
     const int N = L.N;
-    const double *xr = a.x_refs + (size_t)b * a.ref_rows * 3;
-    const double *ur = a.u_refs + (size_t)b * a.uref_rows * 2;
+    const double *xr = a.x_refs + ref_row0(a.prm.ref_off, b, a.ref_rows) * 3;
+    const double *ur = a.u_refs + ref_row0(a.prm.ref_off, b, a.uref_rows) * 2;
     double corr = 0.0, prev = xr[2];
     double th0 = xr[2];
     for (int k = 0; k <= N; k++) {
@@ -131,8 +131,8 @@ __device__ void setup_lti(const MpcArgs<T> &a, const WaveTile<T> &w, int64_t b, 
     const MpcLayout &L = a.L;
     const MpcDevParams &p = a.prm;
     const int N = L.N;
-    const double *xr = a.x_refs + (size_t)b * a.ref_rows * 3;
-    const double *ur = a.u_refs + (size_t)b * a.uref_rows * 2;
+    const double *xr = a.x_refs + ref_row0(a.prm.ref_off, b, a.ref_rows) * 3;
+    const double *ur = a.u_refs + ref_row0(a.prm.ref_off, b, a.uref_rows) * 2;
     double v = ur[0];
     double vr = fabs(v) > 0.01 ? v : 0.1;             // :186
     double s, c;
@@ -530,8 +530,8 @@ __global__ __launch_bounds__(256) void mpc_solve_kernel(MpcArgs<T> a) {
     }
     // ---- outputs
     const int N = L.N;
-    const double *xr = a.x_refs + (size_t)b * a.ref_rows * 3;
-    const double *ur = a.u_refs + (size_t)b * a.uref_rows * 2;
+    const double *xr = a.x_refs + ref_row0(a.prm.ref_off, b, a.ref_rows) * 3;
+    const double *ur = a.u_refs + ref_row0(a.prm.ref_off, b, a.uref_rows) * 2;
     double J = 0;
     int used = 0;
     if (finite && it > 0) {

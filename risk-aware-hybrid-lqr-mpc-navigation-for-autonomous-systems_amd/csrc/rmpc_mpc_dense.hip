@@ -187,8 +187,8 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
     const int no = a.no;
     D d(s, lane, no);
     const double dt = p.dt, rho = p.rho;
-    const double *xr = a.x_refs + (size_t)b * a.ref_rows * 3;
-    const double *ur = a.u_refs + (size_t)b * a.uref_rows * 2;
+    const double *xr = a.x_refs + ref_row0(a.prm.ref_off, b, a.ref_rows) * 3;
+    const double *ur = a.u_refs + ref_row0(a.prm.ref_off, b, a.uref_rows) * 2;
     const int ic = d.ic;
     const bool prof_on = a.prof != nullptr;
     unsigned long long tprof = prof_on ? __builtin_amdgcn_s_memtime() : 0ull;

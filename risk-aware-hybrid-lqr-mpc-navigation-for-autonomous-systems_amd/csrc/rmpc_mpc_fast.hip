@@ -147,8 +147,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     const T Q0 = (T)p.Q[0], Q1 = (T)p.Q[1], Q2 = (T)p.Q[2], R0 = (T)p.R[0], R1 = (T)p.R[1];
     const T P0 = (T)p.P[0], P1 = (T)p.P[1], P2 = (T)p.P[2];
     const T vmax = (T)p.v_max, omax = (T)p.omega_max;
-    const double *xr = a.x_refs + (size_t)b * a.ref_rows * 3;
-    const double *ur = a.u_refs + (size_t)b * a.uref_rows * 2;
+    const double *xr = a.x_refs + ref_row0(a.prm.ref_off, b, a.ref_rows) * 3;
+    const double *ur = a.u_refs + ref_row0(a.prm.ref_off, b, a.uref_rows) * 2;
     // per-wave tiles (sized for fp64; fp32 uses half)
     const GainTile<T> gt(a.gains + (size_t)blockIdx.x * NB * 4 * RMPC_WAVE, NB, lane);
     const UsolTile<T> ut(a.usol + (size_t)blockIdx.x * NB * RMPC_WAVE, NB, lane);

@@ -119,8 +119,8 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
     const double P0 = p.P[0], P1 = p.P[1], P2 = p.P[2];
     const double eps_h = SetTol<double>::hinge, eps_b = SetTol<double>::box;
     const int64_t b = have ? (int64_t)a.index[t] : 0;
-    const double *xr = a.x_refs + (size_t)b * a.ref_rows * 3;
-    const double *ur = a.u_refs + (size_t)b * a.uref_rows * 2;
+    const double *xr = a.x_refs + ref_row0(a.prm.ref_off, b, a.ref_rows) * 3;
+    const double *ur = a.u_refs + ref_row0(a.prm.ref_off, b, a.uref_rows) * 2;
     const bool prof_on = a.prof != nullptr;
     unsigned long long tprof = prof_on ? __builtin_amdgcn_s_memtime() : 0ull;
     unsigned long long pacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};

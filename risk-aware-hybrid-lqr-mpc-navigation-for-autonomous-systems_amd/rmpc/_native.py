@@ -11,7 +11,8 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librmpc.so")
+# RMPC_LIB_PATH: load an alternative build of the library (A/B diagnostics only)
+LIB_PATH = os.environ.get("RMPC_LIB_PATH") or os.path.join(_HERE, "librmpc.so")
 
 RMPC_OK = 0
 RMPC_OPTIMAL, RMPC_OPTIMAL_INACCURATE, RMPC_FALLBACK, RMPC_DARE_FALLBACK = 0, 1, 2, 3

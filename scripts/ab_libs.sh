@@ -1,0 +1,13 @@
+#!/bin/bash
+# A/B of alternative library builds (rmpc/librmpc_<name>.so): cfg3 bench value + fast/tail
+# per-phase counters.  Usage: bash scripts/ab_libs.sh name1 name2 ...  ("-" = default build)
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+D=risk-aware-hybrid-lqr-mpc-navigation-for-autonomous-systems_amd/rmpc
+for v in "$@"; do
+  if [ "$v" = "-" ]; then lib=$D/librmpc.so; else lib=$D/librmpc_$v.so; fi
+  echo "== $v"
+  RMPC_LIB_PATH=$PWD/$lib timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pcie > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err || exit $?
+  python -c "import json;d=json.load(open('gpurun_out/ab_$v.json'));print('value %.4e ms/step %.4f'%(d['value'],d['ms_per_step']), d['roofline'].get('stage_ms'), 'iters', d['solver']['iters_mean'], 'opt', d['solver']['optimal'])"
+  RMPC_DENSE_PROF=1 RMPC_LIB_PATH=$PWD/$lib timeout -k 10 200 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-pcie > /dev/null 2> gpurun_out/ab_${v}_prof.err || exit $?
+  grep "\[fast\]" gpurun_out/ab_${v}_prof.err | tail -1
+done

@@ -1,0 +1,11 @@
+#!/bin/bash
+# GPU parity suite, then a short cfg3 bench + per-phase counters (RMPC_DENSE_PROF) of the
+# fast and tail kernels.  Usage: bash scripts/quick.sh <tag> [extra env assignments...]
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+tag=${1:-q}; shift
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -W ignore > gpurun_out/${tag}_tests.log 2>&1
+rc=$?; tail -2 gpurun_out/${tag}_tests.log; [ $rc -ne 0 ] && { tail -40 gpurun_out/${tag}_tests.log; exit $rc; }
+env "$@" timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pcie > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || exit $?
+python -c "import json;d=json.load(open('gpurun_out/${tag}_bench.json'));print('value %.4e ms/step %.4f'%(d['value'],d['ms_per_step']), d['roofline'].get('stage_ms'), d['solver'])"
+env RMPC_DENSE_PROF=1 "$@" timeout -k 10 200 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-pcie > /dev/null 2> gpurun_out/${tag}_prof.err || exit $?
+grep "\[group\]\|\[fast\]\|\[dense\]" gpurun_out/${tag}_prof.err | tail -3

@@ -419,6 +419,26 @@ def test_rollout_hybrid_matches_oracle_closed_loop(rm):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["lqr", "mpc", "hybrid"])
+def test_rollout_shared_table_refs_equal_copied_segments(rm, monkeypatch, mode):
+    """rollouts read each robot's reference segment straight from one
+    shared, end-padded Figure-8 table (per-robot row offsets) instead of per-step copies.
+    Same rows, so the closed loops must be bit-identical, including robots that run past
+    the table end (get_trajectory_segment's clamp, reference_generator.py:299-326)."""
+    lp = rm._native.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0)
+    mp = rm._native.mpc_params(20, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                               0.02, block_size=1)
+    rp = rm._native.risk_params()
+    starts = np.concatenate([np.arange(0, 999, 13), [960, 985, 999]]).astype(np.int32)
+    kw = dict(lparams=lp, mparams=mp, rparams=rp, start_index=starts,
+              obstacles=ompc.default_obstacles())
+    shared = rm.batch.rollout_batch(mode, 50, **kw)
+    monkeypatch.setenv("RMPC_ROLLOUT_REFS", "copy")
+    copied = rm.batch.rollout_batch(mode, 50, **kw)
+    for key in ("states", "controls", "used_mpc", "mpc_status"):
+        np.testing.assert_array_equal(shared[key], copied[key])
+
+
 def test_rollout_batch_is_independent_per_robot(rm):
     """A robot's rollout does not depend on the batch it is in (no cross-robot coupling)."""
     lp = rm._native.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0)
