@@ -315,7 +315,6 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         // default cap (sweeps with the lane-group tail): 7 at N <= 20 (BASELINE config 3), 12
         // beyond (config 4)
         a.pdas_cap = getenv("RMPC_FAST_CAP") ? atoi(getenv("RMPC_FAST_CAP")) : (p->horizon <= 20 ? 7 : 12);
-        a.screen = !getenv("RMPC_NO_SCREEN");
         const bool warm = !getenv("RMPC_COLD_TAIL");
         if (warm) {
             HIP_TRY(c->retry_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));

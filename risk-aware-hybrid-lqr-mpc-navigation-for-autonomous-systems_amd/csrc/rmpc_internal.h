@@ -52,7 +52,6 @@ struct MpcFastArgs {
     const int32_t *index, *count;    // optional robot index list (device-side length)
     int32_t *retry, *retry_count;    // robots handed to the next stage
     int pdas_cap;                    // PDAS solves before a robot is handed on
-    int screen;                      // forward-sweep row screening on (RMPC_NO_SCREEN=1: off)
     unsigned long long *prof;        // diagnostics: per-phase cycle counters (may be null)
     uint32_t *retry_sets;            // per retry slot: hinge flags [N], box states [NB], iters
                                      // (warm start of the next stage; may be null)
