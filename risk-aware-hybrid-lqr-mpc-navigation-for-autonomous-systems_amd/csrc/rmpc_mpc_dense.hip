@@ -718,18 +718,18 @@ __device__ __forceinline__ void dense_solve(const DenseArgs &a, double *s, int t
     }
 }
 
-// Persistent: each workgroup takes the next list entry from a device counter until the
-// list (length written by the fast kernel earlier on the same stream) is exhausted --
-// dynamic, because per-robot cost varies by 10x and more.
+// One list entry per workgroup (one wave), one round: the grid covers the list's capacity
+// and workgroups past the device-side count (written by the fast kernel earlier on the same
+// stream) exit at once.  No persistent round loop: the lane-group tail's equivalent faulted
+// from its second round on (rmpc_mpc_group.hip), so neither tail loops over rounds.
 template <int N, int BS>
 __global__ __launch_bounds__(64, 1) void mpc_dense_kernel(DenseArgs a) {
     extern __shared__ double s[];
     const int lane = threadIdx.x;
     const int cnt = *a.count;
-    for (int t = blockIdx.x; t < cnt; t += gridDim.x) {
-        __syncthreads();                // LDS of the previous robot is dead
-        dense_solve<N, BS>(a, s, t, lane);
-    }
+    const int t = blockIdx.x;
+    if (t >= cnt) return;
+    dense_solve<N, BS>(a, s, t, lane);
 }
 
 }  // namespace rmpc
@@ -765,11 +765,7 @@ hipError_t rmpc_launch_mpc_dense_f64(const MpcDevParams &prm, int N, int bs, int
     a.warm = warm;
     a.pdas_cap = pdas_cap < RMPC_PDAS_ITERS ? pdas_cap : RMPC_PDAS_ITERS;
     const size_t lds = (size_t)dense_lds_doubles(N, bs, no) * sizeof(double);
-    // one wave per SIMD (VGPR-bound): 4 per CU fill the chip, more only queue
-    const int per_cu = getenv("RMPC_DENSE_WPC") ? atoi(getenv("RMPC_DENSE_WPC")) : 4;
-    const int64_t gmax = (int64_t)256 * (per_cu > 0 ? per_cu : 4);
-    const int64_t grid = capacity < gmax ? capacity : gmax;
-    const dim3 g((unsigned)grid), blk(64);
+    const dim3 g((unsigned)capacity), blk(64);
     const void *fn = (bs == 1 && N == 30)   ? (const void *)mpc_dense_kernel<30, 1>
                      : (bs == 1 && N == 20) ? (const void *)mpc_dense_kernel<20, 1>
                      : (bs == 1 && N == 10) ? (const void *)mpc_dense_kernel<10, 1>

@@ -26,6 +26,7 @@
 #include "rmpc_internal.h"
 #include "rmpc_riccati.h"
 
+#include <cstdio>
 #include <cstdlib>
 
 namespace rmpc {
@@ -44,7 +45,16 @@ struct GroupArgs {
     const uint32_t *warm;             // per list entry: hinge flags [N], box states [NB], iters
     int pdas_cap;                     // PDAS solves before projected Newton
     unsigned long long *prof;         // optional per-phase cycle counters (diagnostics)
+    int64_t nB;                       // rows of the per-robot output arrays (bounds checks)
+    int32_t *chk;                     // optional bounds-check flags (RMPC_GROUP_CHECK)
 };
+
+// retry-list append with an optional bounds check
+__device__ __forceinline__ void group_retry(const GroupArgs &a, int64_t b) {
+    const int slot = atomicAdd(a.retry_count, 1);
+    if (a.chk && (slot < 0 || slot >= a.nB)) { atomicOr(a.chk, 4); return; }
+    a.retry[slot] = (int32_t)b;
+}
 
 // diagnostics: s_memtime deltas per phase (wave-uniform), flushed once per robot round
 #define GPROF(slot)                                                                   \
@@ -101,10 +111,11 @@ __device__ __forceinline__ double gmaxv(double v) {
 
 enum { PH_PDAS = 0, PH_PN = 1, PH_DONE = 2, PH_IDLE = 3 };
 
-// Stores from inside the uniform recursions: the group's first lane writes the record, the
-// others a private junk slot -- a select of two provably disjoint addresses instead of a
-// branch, so the sweep stays one basic block and the scheduler can issue the next steps'
-// LDS loads ahead of these stores.
+// Stores from inside the uniform recursions: all lanes of a group hold identical values, so
+// all of them store (no branch, no address select: the sweep stays one basic block and
+// the scheduler can issue the next steps' LDS loads ahead of these stores; the plain
+// stores took 7% off the tail launch against the former lane-0-or-junk-slot select).
+// Stores that only some groups may make (GSTM) select a private junk slot instead.
 __shared__ double grp_junk[64];
 
 template <int N, int BS, int G>
@@ -118,7 +129,8 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
     const double Q0 = p.Q[0], Q1 = p.Q[1], Q2 = p.Q[2], R0 = p.R[0], R1 = p.R[1];
     const double P0 = p.P[0], P1 = p.P[1], P2 = p.P[2];
     const double eps_h = SetTol<double>::hinge, eps_b = SetTol<double>::box;
-    const int64_t b = have ? (int64_t)a.index[t] : 0;
+    int64_t b = have ? (int64_t)a.index[t] : 0;
+    if (a.chk && have && (b < 0 || b >= a.nB)) { atomicOr(a.chk, 1); b = 0; have = false; }
     const double *xr = a.x_refs + ref_row0(a.prm.ref_off, b, a.ref_rows) * 3;
     const double *ur = a.u_refs + ref_row0(a.prm.ref_off, b, a.uref_rows) * 2;
     const bool prof_on = a.prof != nullptr;
@@ -129,7 +141,9 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
     // cannot hoist the (loop-invariant) per-step data out of the iteration loop
     double *base = base0;
     double *const junk = grp_junk + threadIdx.x;
-#define GST(ref, v) (*(gl == 0 ? &(ref) : junk) = (v))
+// GST: every lane of the group stores its (bitwise identical) copy -- no address select;
+// GSTM: masked per group through the junk slot (groups whose values are not meaningful)
+#define GST(ref, v) ((ref) = (v))
 #define GSTM(ref, v, m) (*((m) && gl == 0 ? &(ref) : junk) = (v))
     auto refresh = [&]() __attribute__((always_inline)) {
         int o = 0;
@@ -222,7 +236,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
     GPROF(0);
     int phase = have ? PH_PDAS : PH_IDLE;
     if (gany<G>(have && !fin, grp)) {                 // fallback law: the generic kernel owns it
-        if (gl == 0) a.retry[atomicAdd(a.retry_count, 1)] = (int32_t)b;
+        if (gl == 0) group_retry(a, b);
         phase = PH_IDLE;
     }
 
@@ -390,7 +404,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
             const double u1v = bf1 == 0 ? e1 : (bf1 == 1 ? lo1 : hi1);
             const int ns0 = box_rule_bf(bf0, e0, lo0, hi0, eps_b), ns1 = box_rule_bf(bf1, e1, lo1, hi1, eps_b);
             bchg = bchg || ns0 != bf0 || ns1 != bf1;
-            *(gl == 0 ? &NBF(j) : reinterpret_cast<uint32_t *>(junk)) = (uint32_t)(ns0 | (ns1 << 2));
+            NBF(j) = (uint32_t)(ns0 | (ns1 << 2));
             GST(ZC(2 * j), u0v);
             GST(ZC(2 * j + 1), u1v);
 #pragma unroll
@@ -557,7 +571,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
                     if (a.iters) a.iters[b] = it0 + it;
                 }
             } else if (cert && gl == 0) {
-                a.retry[atomicAdd(a.retry_count, 1)] = (int32_t)b;
+                group_retry(a, b);
             }
             __syncthreads();
             GPROF(6);
@@ -631,7 +645,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
         if (prof_on) pacc[9]++;
         if (phase == PH_PN && !cert && it >= max_iter) fail = true;
         if (fail) {
-            if (gl == 0) a.retry[atomicAdd(a.retry_count, 1)] = (int32_t)b;
+            if (gl == 0) group_retry(a, b);
             phase = PH_IDLE;
         }
         if (prof_on && gl == 0 && (cert || fail))   // per robot: tail iterations (histogram)
@@ -662,7 +676,11 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
 #undef GSTM
 }
 
-// Persistent over rounds of 64/G list entries per wave; one wave per workgroup.
+// One wave per workgroup, 64/G list entries per wave, one round: the grid covers the list's
+// capacity and waves past the device-side count exit at once (measured free next to the
+// tail's run time).  A persistent variant that looped over rounds faulted from its second
+// round on (every robot's accesses in bounds, checked with RMPC_GROUP_CHECK), so there is
+// no round loop.
 template <int N, int BS, int G>
 __global__ __launch_bounds__(64, 1) void mpc_group_kernel(GroupArgs a) {
     constexpr int NB = (N + BS - 1) / BS, RPW = 64 / G;
@@ -670,11 +688,11 @@ __global__ __launch_bounds__(64, 1) void mpc_group_kernel(GroupArgs a) {
     const int lane = threadIdx.x, gl = lane % G, grp = lane / G;
     const int rec = GRec<N, NB>::size(a.no);
     const int cnt = *a.count;
-    for (int t0 = blockIdx.x * RPW; t0 < cnt; t0 += gridDim.x * RPW) {
-        const int t = t0 + grp;
-        group_solve<N, BS, G>(a, lds + grp * rec, t, t < cnt, gl, grp);
-        __syncthreads();
-    }
+    if (a.chk && lane == 0 && blockIdx.x == 0 && (cnt < 0 || cnt > a.nB)) atomicOr(a.chk, 2);
+    const int t0 = blockIdx.x * RPW;
+    if (t0 >= cnt) return;
+    const int t = t0 + grp;
+    group_solve<N, BS, G>(a, lds + grp * rec, t, t < cnt, gl, grp);
 }
 
 // lanes per robot: 16 (four robots per wave) while the record leaves room for four waves
@@ -723,13 +741,23 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
     a.index = index; a.count = count; a.retry = retry; a.retry_count = retry_count;
     a.warm = warm;
     a.prof = prof;
+    a.nB = capacity;
+    a.chk = nullptr;
+    static int32_t *chk = nullptr;                // RMPC_GROUP_CHECK=1: bounds-check flags
+    if (getenv("RMPC_GROUP_CHECK")) {
+        if (!chk) {
+            const hipError_t e = hipMalloc((void **)&chk, sizeof(int32_t));
+            if (e != hipSuccess) return e;
+        }
+        const hipError_t e = hipMemsetAsync(chk, 0, sizeof(int32_t), stream);
+        if (e != hipSuccess) return e;
+        a.chk = chk;
+    }
     a.pdas_cap = pdas_cap < RMPC_PDAS_ITERS ? pdas_cap : RMPC_PDAS_ITERS;
     const int G = group_lanes(N, bs), rpw = 64 / G;
     const size_t lds = (size_t)rpw * group_rec(N, bs, no) * sizeof(double);
-    const int per_cu = getenv("RMPC_GROUP_WPC") ? atoi(getenv("RMPC_GROUP_WPC")) : 4;
-    const int64_t gmax = (int64_t)256 * (per_cu > 0 ? per_cu : 4);
     const int64_t need = (capacity + rpw - 1) / rpw;
-    const dim3 g((unsigned)(need < gmax ? need : gmax)), blk(64);
+    const dim3 g((unsigned)need), blk(64);
     const void *fn = (bs == 1 && N == 30)   ? (const void *)mpc_group_kernel<30, 1, 32>
                      : (bs == 1 && N == 20) ? (const void *)mpc_group_kernel<20, 1, 16>
                      : (bs == 1 && N == 10) ? (const void *)mpc_group_kernel<10, 1, 16>
@@ -744,5 +772,13 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
     else if (bs == 1 && N == 10) hipLaunchKernelGGL((mpc_group_kernel<10, 1, 16>), g, blk, lds, stream, a);
     else if (bs == 1 && N == 6) hipLaunchKernelGGL((mpc_group_kernel<6, 1, 16>), g, blk, lds, stream, a);
     else hipLaunchKernelGGL((mpc_group_kernel<6, 2, 16>), g, blk, lds, stream, a);
+    if (a.chk) {
+        int32_t h = 0;
+        hipError_t e = hipMemcpyAsync(&h, a.chk, sizeof(h), hipMemcpyDeviceToHost, stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream);
+        fprintf(stderr, "[group check] flags %d (1 robot index, 2 list count, 4 retry slot) launch: %s\n", h,
+                hipGetErrorString(e));
+        if (e != hipSuccess) return e;
+    }
     return hipGetLastError();
 }

@@ -222,6 +222,29 @@ def test_mpc_full_config3_vs_cpu_port(rm):
     assert np.array_equal(out["slack_used"][ok], ref["slack_used"][ok])
 
 
+@pytest.mark.parametrize("tail", ["group", "dense"])
+def test_mpc_tail_only_full_batch(rm, monkeypatch, tail):
+    """RMPC_FAST_CAP=0: every one of BASELINE config 3's 65536 robots goes through the tail
+    kernel (16384 lane-group waves / 65536 dense waves, far more than the chip holds at once)
+    -- same results as the C port.  Regression test for the persistent round loop the tails
+    used to have, which faulted from its second round on."""
+    monkeypatch.setenv("RMPC_FAST_CAP", "0")
+    if tail == "dense":
+        monkeypatch.setenv("RMPC_TAIL", "dense")
+    B, N = 65536, 20
+    t0 = (np.arange(B) / B) * (2 * np.pi / 0.5)
+    x0, xr, ur = _workload(N, B, 1, t0=t0)
+    obs = ompc.default_obstacles()
+    p = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+    out = rm.batch.mpc_solve_batch(p, x0, xr, ur, obs)
+    cp = cpu.mpc_params(N, (15, 15, 50), (.1, .1), (30, 30, 40), 0.3, 5000., 2., 3., 0.02)
+    ref = cpu.mpc_solve_batch(cp, x0, xr, ur, obs, threads=8)
+    ok = (out["status"] == 0) & (ref["status"] == 0)
+    assert ok.mean() >= 0.9999
+    d = np.abs(out["u_seq"] - ref["u_seq"]).max(axis=(1, 2))
+    assert np.all(d[ok] <= 1e-9), d.max()
+
+
 def test_mpc_edge_cases(rm):
     obs = ompc.default_obstacles()
     oc = ompc.MPCController(6, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
