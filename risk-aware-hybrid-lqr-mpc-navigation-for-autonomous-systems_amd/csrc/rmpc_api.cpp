@@ -340,7 +340,8 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         // (RMPC_TAIL=dense); RMPC_DISABLE_DENSE skips the tail stage altogether
         const char *tail = getenv("RMPC_TAIL");
         const bool use_dense = tail && !strcmp(tail, "dense");
-        const int tail_cap = getenv("RMPC_DENSE_CAP") ? atoi(getenv("RMPC_DENSE_CAP")) : 4;
+        // tail PDAS cap before projected Newton (sweeps: 4 at N <= 20, 6 beyond -- config 4)
+        const int tail_cap = getenv("RMPC_DENSE_CAP") ? atoi(getenv("RMPC_DENSE_CAP")) : (p->horizon <= 20 ? 4 : 6);
         if (!use_dense && rmpc_mpc_group_supported(p->horizon, bs, n_obs) && !getenv("RMPC_DISABLE_DENSE")) {
             HIP_TRY(c->retry2.ensure((size_t)B * sizeof(int32_t)));
             int32_t *cnt2 = (int32_t *)c->retry_count.p + 8;

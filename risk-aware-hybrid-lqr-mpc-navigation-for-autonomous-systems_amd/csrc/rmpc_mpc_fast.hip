@@ -231,15 +231,18 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                     for (int o = 0; o < no; o++) {      // branch-free: inactive rows add 0
                         // obstacle o+1 loads while row o computes (LDS latency off the row chain)
                         const T nx = obs_s[3 * o + 3], ny = obs_s[3 * o + 4], ns = obs_s[3 * o + 5];
-                        T n0, n1, hb;
-                        hinge_row_fast(px, py, cx, cy, cs, n0, n1, hb);
+                        // fp64: skip a row no lane of the wave has active (wave-uniform branch)
+                        if (!F64 || __builtin_amdgcn_ballot_w64(((Hf[k] >> o) & 1u) != 0u)) {
+                            T n0, n1, hb;
+                            hinge_row_fast(px, py, cx, cy, cs, n0, n1, hb);
+                            const T w = ((Hf[k] >> o) & 1u) ? rho : (T)0;
+                            q00 += w * n0 * n0;
+                            q01 += w * n0 * n1;
+                            q11 += w * n1 * n1;
+                            qv0 -= w * hb * n0;
+                            qv1 -= w * hb * n1;
+                        }
                         cx = nx; cy = ny; cs = ns;
-                        const T w = ((Hf[k] >> o) & 1u) ? rho : (T)0;
-                        q00 += w * n0 * n0;
-                        q01 += w * n0 * n1;
-                        q11 += w * n1 * n1;
-                        qv0 -= w * hb * n0;
-                        qv1 -= w * hb * n1;
                     }
                 }
                 const T vr = fabs(V0[k]) > (T)0.01 ? V0[k] : (T)0.1;     // :425
