@@ -339,7 +339,9 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             const int ns0 = box_rule_bf(bf0, e0, lo0, hi0, eps_b), ns1 = box_rule_bf(bf1, e1, lo1, hi1, eps_b);
             changed |= (int)(ns0 != bf0 || ns1 != bf1);
             Bf[j] = (uint32_t)(ns0 | (ns1 << 2));
+#ifdef RMPC_FAST_USOL
             ut.st(j, u0v, u1v);
+#endif
 #pragma unroll
             for (int k = k0; k < k1; k++) {
                 J += Q0 * x0 * x0 + Q1 * x1 * x1 + Q2 * x2 * x2;
@@ -425,9 +427,30 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
 #pragma unroll
     for (int j = 0; j < NB; j++) {
         T du0, du1;
-        ut.ld(j, du0, du1);
         const int k0 = j * BS;
         const int k1 = (k0 + BS < N) ? k0 + BS : N;
+#ifdef RMPC_FAST_USOL
+        ut.ld(j, du0, du1);
+#else
+        {   // the certified inputs, re-derived from the last backward sweep's gains along the
+            // same trajectory (no per-iteration input tile)
+            T g[8];
+            gt.ld(j, g);
+            T lo0 = -BIG, hi0 = BIG, lo1 = -BIG, hi1 = BIG;
+#pragma unroll
+            for (int k = k0; k < k1; k++) {
+                lo0 = fmax(lo0, -vmax - V0[k]);
+                hi0 = fmin(hi0, vmax - V0[k]);
+                lo1 = fmax(lo1, -omax - V1(k));
+                hi1 = fmin(hi1, omax - V1(k));
+            }
+            const T e0 = g[0] * x0 + g[1] * x1 + g[2] * x2 + g[6];
+            const T e1 = g[3] * x0 + g[4] * x1 + g[5] * x2 + g[7];
+            const int bf0 = Bf[j] & 3, bf1 = (Bf[j] >> 2) & 3;
+            du0 = bf0 == 0 ? e0 : (bf0 == 1 ? lo0 : hi0);
+            du1 = bf1 == 0 ? e1 : (bf1 == 1 ? lo1 : hi1);
+        }
+#endif
 #pragma unroll
         for (int k = k0; k < k1; k++) {
             double v0 = F64 ? (double)(du0 + V0[k]) : (double)du0 + ur[2 * k];

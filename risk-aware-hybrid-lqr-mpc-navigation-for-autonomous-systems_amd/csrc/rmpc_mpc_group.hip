@@ -245,6 +245,31 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
 
     // trajectory under the inputs Z (ZC / ZZ / ZT) -> XS, full objective (constants included,
     // as the fast kernel's J), and whether any hinge residual exceeds 1e-6 (slack_used, :485)
+    // full objective of the inputs at zoff along the trajectory in XS (lane-parallel)
+    auto cost = [&](int zoff, int &used) __attribute__((always_inline)) -> double {
+        refresh();
+        double jl = 0.0;
+        int u = 0;
+        for (int k = gl; k <= N; k += G) {
+            const double y0 = XS(k, 0), y1 = XS(k, 1), y2 = XS(k, 2);
+            if (k == N) {
+                jl += P0 * y0 * y0 + P1 * y1 * y1 + P2 * y2 * y2;
+            } else {
+                jl += Q0 * y0 * y0 + Q1 * y1 * y1 + Q2 * y2 * y2;
+                const int j = k / BS;
+                const double uu0 = base[zoff + 2 * j] + STG(4, k), uu1 = base[zoff + 2 * j + 1] + STG(5, k);
+                jl += R0 * uu0 * uu0 + R1 * uu1 * uu1;
+                for (int o = 0; o < no; o++) {
+                    const double r = HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1;
+                    if (r > 0) jl += rho * r * r;
+                    u |= (r > 1e-6);
+                }
+            }
+        }
+        used = gany<G>(u, grp);
+        return gsum<G>(jl);
+    };
+
     auto objective = [&](int zoff, bool m, int &used) __attribute__((always_inline)) -> double {
         refresh();
         double x0 = d0, x1 = d1, x2 = d2;
@@ -272,27 +297,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
         }
         GSTM(XS(N, 0), x0, m); GSTM(XS(N, 1), x1, m); GSTM(XS(N, 2), x2, m);
         __syncthreads();
-        refresh();
-        double jl = 0.0;
-        int u = 0;
-        for (int k = gl; k <= N; k += G) {
-            const double y0 = XS(k, 0), y1 = XS(k, 1), y2 = XS(k, 2);
-            if (k == N) {
-                jl += P0 * y0 * y0 + P1 * y1 * y1 + P2 * y2 * y2;
-            } else {
-                jl += Q0 * y0 * y0 + Q1 * y1 * y1 + Q2 * y2 * y2;
-                const int j = k / BS;
-                const double uu0 = base[zoff + 2 * j] + STG(4, k), uu1 = base[zoff + 2 * j + 1] + STG(5, k);
-                jl += R0 * uu0 * uu0 + R1 * uu1 * uu1;
-                for (int o = 0; o < no; o++) {
-                    const double r = HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1;
-                    if (r > 0) jl += rho * r * r;
-                    u |= (r > 1e-6);
-                }
-            }
-        }
-        used = gany<G>(u, grp);
-        return gsum<G>(jl);
+        return cost(zoff, used);
     };
 
     // the quadratic piece of the current sets (HF, BF; fixed components at their bounds):
@@ -533,8 +538,9 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
         const bool cert = act && !chg;
         if (__any(cert)) {
             // ---- outputs from the certified candidate (mpc_controller.py:484-520)
+            // the certifying solve's forward sweep left ZC's trajectory in XS: no re-simulation
             int used = 0;
-            const double J = objective(RC::ZC, cert, used);
+            const double J = cost(RC::ZC, used);
             refresh();
             if (cert && isfinite(J)) {
                 const int sc = a.step_count ? a.step_count[b] : 0;
