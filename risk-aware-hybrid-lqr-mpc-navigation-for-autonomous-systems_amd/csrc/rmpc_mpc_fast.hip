@@ -112,6 +112,27 @@ template <> struct UsolTile<float> {
     }
 };
 
+// Active-set flags packed into few VGPRs (the kernel runs at the register limit; the
+// sweeps are fully unrolled, so every index is a compile-time constant and a get/set is one
+// or two shift/mask instructions).  Hinge rows: 16 bits per step (bit o); box states:
+// 4 bits per block (bits 0-1 component 0, bits 2-3 component 1).
+template <int N> struct HingeFlags {
+    uint32_t w[(N + 1) / 2];
+    __device__ __forceinline__ uint32_t get(int k) const { return (w[k >> 1] >> (16 * (k & 1))) & 0xffffu; }
+    __device__ __forceinline__ void set(int k, uint32_t v) {
+        const int sh = 16 * (k & 1);
+        w[k >> 1] = (w[k >> 1] & ~(0xffffu << sh)) | (v << sh);
+    }
+};
+template <int NB> struct BoxFlags {
+    uint32_t w[(NB + 7) / 8];
+    __device__ __forceinline__ uint32_t get(int j) const { return (w[j >> 3] >> (4 * (j & 7))) & 0xfu; }
+    __device__ __forceinline__ void set(int j, uint32_t v) {
+        const int sh = 4 * (j & 7);
+        w[j >> 3] = (w[j >> 3] & ~(0xfu << sh)) | (v << sh);
+    }
+};
+
 template <typename T> struct Big;
 template <> struct Big<double> { static constexpr double v = 1e300; };
 template <> struct Big<float> { static constexpr float v = 1e30f; };
@@ -188,12 +209,12 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     const T d0 = (T)(x0p[0] - xr[0]), d1 = (T)(x0p[1] - xr[1]), d2 = (T)(x0a - th0);
     fin = fin && isfinite(d0 + d1 + d2);
 
-    uint32_t Hf[N];                   // hinge-row active flags of step k (bit o)
-    uint32_t Bf[NB];                  // box state per block: bits 0-1 comp 0, bits 2-3 comp 1
+    HingeFlags<N> Hf;                 // hinge-row active flags of step k (bit o)
+    BoxFlags<NB> Bf;                  // box state per block
 #pragma unroll
-    for (int k = 0; k < N; k++) Hf[k] = 0;
+    for (int i = 0; i < (N + 1) / 2; i++) Hf.w[i] = 0;
 #pragma unroll
-    for (int j = 0; j < NB; j++) Bf[j] = 0;
+    for (int i = 0; i < (NB + 7) / 8; i++) Bf.w[i] = 0;
 
     int it = 0, cert = 0, used = 0;
     T J = 0;
@@ -225,17 +246,17 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                 const int k = j;
                 T q00 = Q0, q01 = 0, q11 = Q1;
                 T qv0 = -Q0 * (T)0, qv1 = -Q1 * (T)0, qv2 = -Q2 * (T)0;
-                if (k > 0 && Hf[k]) {
+                if (k > 0 && Hf.get(k)) {
                     const T px = PX(k), py = PY(k);
                     T cx = obs_s[0], cy = obs_s[1], cs = obs_s[2];
                     for (int o = 0; o < no; o++) {      // branch-free: inactive rows add 0
                         // obstacle o+1 loads while row o computes (LDS latency off the row chain)
                         const T nx = obs_s[3 * o + 3], ny = obs_s[3 * o + 4], ns = obs_s[3 * o + 5];
                         // fp64: skip a row no lane of the wave has active (wave-uniform branch)
-                        if (!F64 || __builtin_amdgcn_ballot_w64(((Hf[k] >> o) & 1u) != 0u)) {
+                        if (!F64 || __builtin_amdgcn_ballot_w64(((Hf.get(k) >> o) & 1u) != 0u)) {
                             T n0, n1, hb;
                             hinge_row_fast(px, py, cx, cy, cs, n0, n1, hb);
-                            const T w = ((Hf[k] >> o) & 1u) ? rho : (T)0;
+                            const T w = ((Hf.get(k) >> o) & 1u) ? rho : (T)0;
                             q00 += w * n0 * n0;
                             q01 += w * n0 * n1;
                             q11 += w * n1 * n1;
@@ -250,7 +271,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                 const T b0 = Cs[k] * dt, b1 = S[k] * dt;
                 const T lo0 = -vmax - V0[k], hi0 = vmax - V0[k];       // :431-436
                 const T lo1 = -omax - V1(k), hi1 = omax - V1(k);
-                const int bf0 = Bf[j] & 3, bf1 = (Bf[j] >> 2) & 3;
+                const uint32_t bfj = Bf.get(j);
+                const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
                 V = ric_step1_bf(V, a0, a1, b0, b1, dt, q00, q01, q11, Q2, qv0, qv1, qv2, R0, R1,
                                  R0 * V0[k], R1 * V1(k), bf0, bf1, bf0 == 1 ? lo0 : hi0, bf1 == 1 ? lo1 : hi1, G);
             } else {
@@ -260,7 +282,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                 for (int k = k1 - 1; k >= k0; k--) {
                     T q00 = Q0, q01 = 0, q11 = Q1;
                     T qv0 = -Q0 * (T)0, qv1 = -Q1 * (T)0, qv2 = -Q2 * (T)0;
-                    if (k > 0 && Hf[k]) {
+                    if (k > 0 && Hf.get(k)) {
                         const T px = PX(k), py = PY(k);
                         T cx = obs_s[0], cy = obs_s[1], cs = obs_s[2];
                         for (int o = 0; o < no; o++) {      // branch-free: inactive rows add 0
@@ -268,7 +290,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                             T n0, n1, hb;
                             hinge_row_fast(px, py, cx, cy, cs, n0, n1, hb);
                             cx = nx; cy = ny; cs = ns;
-                            const T w = ((Hf[k] >> o) & 1u) ? rho : (T)0;
+                            const T w = ((Hf.get(k) >> o) & 1u) ? rho : (T)0;
                             q00 += w * n0 * n0;
                             q01 += w * n0 * n1;
                             q11 += w * n1 * n1;
@@ -290,7 +312,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                     lo1 = fmax(lo1, -omax - V1(k));
                     hi1 = fmin(hi1, omax - V1(k));
                 }
-                const int bf0 = Bf[j] & 3, bf1 = (Bf[j] >> 2) & 3;
+                const uint32_t bfj = Bf.get(j);
+                const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
                 V = ric_block_bf(W, bf0, bf1, bf0 == 1 ? lo0 : hi0, bf1 == 1 ? lo1 : hi1, G);
             }
             gt.st(j, G);
@@ -333,12 +356,13 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             }
             const T e0 = g[j][0] * x0 + g[j][1] * x1 + g[j][2] * x2 + g[j][6];
             const T e1 = g[j][3] * x0 + g[j][4] * x1 + g[j][5] * x2 + g[j][7];
-            const int bf0 = Bf[j] & 3, bf1 = (Bf[j] >> 2) & 3;
+            const uint32_t bfj = Bf.get(j);
+                const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
             const T u0v = bf0 == 0 ? e0 : (bf0 == 1 ? lo0 : hi0);
             const T u1v = bf1 == 0 ? e1 : (bf1 == 1 ? lo1 : hi1);
             const int ns0 = box_rule_bf(bf0, e0, lo0, hi0, eps_b), ns1 = box_rule_bf(bf1, e1, lo1, hi1, eps_b);
             changed |= (int)(ns0 != bf0 || ns1 != bf1);
-            Bf[j] = (uint32_t)(ns0 | (ns1 << 2));
+            Bf.set(j, (uint32_t)(ns0 | (ns1 << 2)));
 #ifdef RMPC_FAST_USOL
             ut.st(j, u0v, u1v);
 #endif
@@ -347,7 +371,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                 J += Q0 * x0 * x0 + Q1 * x1 * x1 + Q2 * x2 * x2;
                 const T uu0 = u0v + V0[k], uu1 = u1v + V1(k);
                 J += R0 * uu0 * uu0 + R1 * uu1 * uu1;
-                uint32_t hk = Hf[k];
+                uint32_t hk = Hf.get(k);
                 const T px = PX(k), py = PY(k);
                 T cx = obs_s[0], cy = obs_s[1], cs = obs_s[2];
                 for (int o = 0; o < no; o++) {          // branch-free row update
@@ -366,7 +390,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                         hk ^= (na ^ act) << o;
                     }
                 }
-                Hf[k] = hk;
+                Hf.set(k, hk);
                 const T vr = fabs(V0[k]) > (T)0.01 ? V0[k] : (T)0.1;
                 const T n0 = x0 + (-vr * S[k] * dt) * x2 + (Cs[k] * dt) * u0v;
                 const T n1 = x1 + (vr * Cs[k] * dt) * x2 + (S[k] * dt) * u0v;
@@ -382,9 +406,9 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         // projected-Newton phase of the next stage
         uint64_t sig = 1469598103934665603ull;
 #pragma unroll
-        for (int k = 0; k < N; k++) sig = (sig ^ (uint64_t)Hf[k]) * 1099511628211ull;
+        for (int i = 0; i < (N + 1) / 2; i++) sig = (sig ^ (uint64_t)Hf.w[i]) * 1099511628211ull;
 #pragma unroll
-        for (int j = 0; j < NB; j++) sig = (sig ^ (uint64_t)Bf[j]) * 1099511628211ull;
+        for (int i = 0; i < (NB + 7) / 8; i++) sig = (sig ^ (uint64_t)Bf.w[i]) * 1099511628211ull;
         if (sig == hist0 || sig == hist1 || sig == hist2 || sig == hist3) break;
         hist3 = hist2; hist2 = hist1; hist1 = hist0; hist0 = sig;
     }
@@ -409,9 +433,9 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         if (a.retry_sets) {                                   // ... from this active set
             uint32_t *ws = a.retry_sets + (size_t)slot * (N + NB + 1);
 #pragma unroll
-            for (int k = 0; k < N; k++) ws[k] = Hf[k];
+            for (int k = 0; k < N; k++) ws[k] = Hf.get(k);
 #pragma unroll
-            for (int j = 0; j < NB; j++) ws[N + j] = Bf[j];
+            for (int j = 0; j < NB; j++) ws[N + j] = Bf.get(j);
             ws[N + NB] = (uint32_t)it;
         }
         return;
@@ -446,7 +470,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             }
             const T e0 = g[0] * x0 + g[1] * x1 + g[2] * x2 + g[6];
             const T e1 = g[3] * x0 + g[4] * x1 + g[5] * x2 + g[7];
-            const int bf0 = Bf[j] & 3, bf1 = (Bf[j] >> 2) & 3;
+            const uint32_t bfj = Bf.get(j);
+                const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
             du0 = bf0 == 0 ? e0 : (bf0 == 1 ? lo0 : hi0);
             du1 = bf1 == 0 ? e1 : (bf1 == 1 ? lo1 : hi1);
         }
