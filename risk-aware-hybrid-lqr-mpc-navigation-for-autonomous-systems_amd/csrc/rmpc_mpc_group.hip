@@ -45,6 +45,7 @@ struct GroupArgs {
     const uint32_t *warm;             // per list entry: hinge flags [N], box states [NB], iters
     int pdas_cap;                     // PDAS solves before projected Newton
     unsigned long long *prof;         // optional per-phase cycle counters (diagnostics)
+    unsigned long long *prof_waves;   // optional per-wave phase records (RMPC_DENSE_PROF=2)
     int64_t nB;                       // rows of the per-robot output arrays (bounds checks)
     int32_t *chk;                     // optional bounds-check flags (RMPC_GROUP_CHECK)
 };
@@ -80,7 +81,9 @@ struct GRec {
     static constexpr int ZT = ZZ + 2 * NB;         // line-search trial point
     static constexpr int GR = ZT + 2 * NB;         // gradient at ZZ
     static constexpr int FR = GR + 2 * NB;         // hinge forces per step [N][2]
-    static constexpr int INT = FR + 2 * N;         // uint32: HF [N], BF [NB], NHF [N], NBF [NB]
+    static constexpr int ZF = FR + 2 * N;          // certified inputs, kept for the final write [2NB]
+    static constexpr int XF = ZF + 2 * NB;         // certified trajectory [N+1][3]
+    static constexpr int INT = XF + 3 * (N + 1);   // uint32: HF [N], BF [NB], NHF [N], NBF [NB]
     static constexpr int HR = INT + (N + NB + 1) / 2 * 2;   // hinge rows [3][no][N] (runtime no)
     __host__ __device__ static int size(int no) {
         const int o = HR + 3 * no * N;
@@ -135,6 +138,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
     const double *ur = a.u_refs + ref_row0(a.prm.ref_off, b, a.uref_rows) * 2;
     const bool prof_on = a.prof != nullptr;
     unsigned long long tprof = prof_on ? __builtin_amdgcn_s_memtime() : 0ull;
+    const unsigned long long tstart = tprof;
     unsigned long long pacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
     // LDS views, re-derived from an opaque offset before each use so that the optimiser
@@ -164,6 +168,8 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
 #define ZT(i) base[RC::ZT + (i)]
 #define GR(i) base[RC::GR + (i)]
 #define FR(c, k) base[RC::FR + 2 * (k) + (c)]
+#define ZF(i) base[RC::ZF + (i)]
+#define XF(k, d) base[RC::XF + 3 * (k) + (d)]
 #define HF(k) reinterpret_cast<uint32_t *>(base + RC::INT)[(k)]
 #define BF(j) reinterpret_cast<uint32_t *>(base + RC::INT)[N + (j)]
 #define NHF(k) reinterpret_cast<uint32_t *>(base + RC::INT)[N + NB + (k)]
@@ -490,6 +496,9 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
     };
 
     // ---- the iteration loop (groups in lockstep)
+    bool done_ok = false;             // certified with a finite objective: written after the loop
+    double J_out = 0.0;
+    int used_out = 0, it_out = 0;
     int it = 0, cyc = 0;
     double F = 0.0;
     uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
@@ -537,45 +546,21 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
         const bool chg = solve_test();
         const bool cert = act && !chg;
         if (__any(cert)) {
-            // ---- outputs from the certified candidate (mpc_controller.py:484-520)
-            // the certifying solve's forward sweep left ZC's trajectory in XS: no re-simulation
+            // ---- certified: objective of the candidate (its trajectory is in XS from the
+            // certifying solve's forward sweep), and a copy of inputs + trajectory kept for
+            // the single output write after the loop (later sweeps overwrite ZC / XS)
             int used = 0;
             const double J = cost(RC::ZC, used);
             refresh();
             if (cert && isfinite(J)) {
-                const int sc = a.step_count ? a.step_count[b] : 0;
-                for (int k = gl; k < N; k += G) {
-                    const int j = k / BS;
-                    const double v0 = ZC(2 * j) + STG(4, k);
-                    double v1 = ZC(2 * j + 1) + STG(5, k);
-                    if (k == 0 && sc < p.ramp_up_steps) {                      // :502-505
-                        const double lim = p.omega_max * ((double)(sc + 1) / (double)p.ramp_up_steps);
-                        v1 = clampv(v1, -lim, lim);
-                    }
-                    if (a.u_seq) {
-                        a.u_seq[((size_t)b * N + k) * 2] = v0;
-                        a.u_seq[((size_t)b * N + k) * 2 + 1] = v1;
-                    }
-                    if (k == 0) {
-                        a.u0[2 * b] = v0;
-                        a.u0[2 * b + 1] = v1;
-                    }
+                for (int i = gl; i < 2 * NB; i += G) ZF(i) = ZC(i);
+                for (int k = gl; k <= N; k += G) {
+                    XF(k, 0) = XS(k, 0); XF(k, 1) = XS(k, 1); XF(k, 2) = XS(k, 2);
                 }
-                if (a.x_pred) {                                                 // :497
-                    for (int k = gl; k <= N; k += G) {
-                        double *xp = a.x_pred + ((size_t)b * (N + 1) + k) * 3;
-                        xp[0] = XS(k, 0) + xr[3 * k];
-                        xp[1] = XS(k, 1) + xr[3 * k + 1];
-                        xp[2] = XS(k, 2) + xr[3 * k + 2];
-                    }
-                }
-                if (gl == 0) {
-                    if (a.step_count) a.step_count[b] = sc + 1;                 // :507
-                    if (a.cost) a.cost[b] = J;
-                    if (a.slack_used) a.slack_used[b] = (uint8_t)used;
-                    a.status[b] = RMPC_OPTIMAL;
-                    if (a.iters) a.iters[b] = it0 + it;
-                }
+                done_ok = true;
+                J_out = J;
+                used_out = used;
+                it_out = it0 + it;
             } else if (cert && gl == 0) {
                 group_retry(a, b);
             }
@@ -657,9 +642,53 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
         if (prof_on && gl == 0 && (cert || fail))   // per robot: tail iterations (histogram)
             atomicAdd(a.prof + 24 + min(it, 31), 1ull);
     }
+    // ---- outputs of every certified robot of the wave, once (mpc_controller.py:484-520)
+    if (__any(done_ok)) {
+        refresh();
+        if (done_ok) {
+            const int sc = a.step_count ? a.step_count[b] : 0;
+            for (int k = gl; k < N; k += G) {
+                const int j = k / BS;
+                const double v0 = ZF(2 * j) + STG(4, k);
+                double v1 = ZF(2 * j + 1) + STG(5, k);
+                if (k == 0 && sc < p.ramp_up_steps) {                      // :502-505
+                    const double lim = p.omega_max * ((double)(sc + 1) / (double)p.ramp_up_steps);
+                    v1 = clampv(v1, -lim, lim);
+                }
+                if (a.u_seq) {
+                    a.u_seq[((size_t)b * N + k) * 2] = v0;
+                    a.u_seq[((size_t)b * N + k) * 2 + 1] = v1;
+                }
+                if (k == 0) {
+                    a.u0[2 * b] = v0;
+                    a.u0[2 * b + 1] = v1;
+                }
+            }
+            if (a.x_pred) {                                                 // :497
+                for (int k = gl; k <= N; k += G) {
+                    double *xp = a.x_pred + ((size_t)b * (N + 1) + k) * 3;
+                    xp[0] = XF(k, 0) + xr[3 * k];
+                    xp[1] = XF(k, 1) + xr[3 * k + 1];
+                    xp[2] = XF(k, 2) + xr[3 * k + 2];
+                }
+            }
+            if (gl == 0) {
+                if (a.step_count) a.step_count[b] = sc + 1;                 // :507
+                if (a.cost) a.cost[b] = J_out;
+                if (a.slack_used) a.slack_used[b] = (uint8_t)used_out;
+                a.status[b] = RMPC_OPTIMAL;
+                if (a.iters) a.iters[b] = it_out;
+            }
+        }
+    }
     if (prof_on && gl == 0 && grp == 0) {
         for (int q = 0; q < 10; q++) atomicAdd(a.prof + q, pacc[q]);
         atomicAdd(a.prof + 10, 1ull);
+        if (a.prof_waves) {          // per-wave record: phases, loop iterations, total cycles
+            unsigned long long *r = a.prof_waves + (size_t)blockIdx.x * 16;
+            for (int q = 0; q < 10; q++) r[q] = pacc[q];
+            r[10] = __builtin_amdgcn_s_memtime() - tstart;
+        }
     }
 #undef STG
 #undef BND
@@ -674,6 +703,8 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
 #undef ZT
 #undef GR
 #undef FR
+#undef ZF
+#undef XF
 #undef HF
 #undef BF
 #undef NHF
@@ -747,6 +778,21 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
     a.index = index; a.count = count; a.retry = retry; a.retry_count = retry_count;
     a.warm = warm;
     a.prof = prof;
+    a.prof_waves = nullptr;
+    static unsigned long long *pw = nullptr;
+    static int64_t pw_cap = 0;
+    const int64_t waves_needed = (capacity + 64 / group_lanes(N, bs) - 1) / (64 / group_lanes(N, bs));
+    if (prof && getenv("RMPC_DENSE_PROF") && atoi(getenv("RMPC_DENSE_PROF")) >= 2) {
+        if (pw_cap < waves_needed) {
+            if (pw) (void)hipFree(pw);
+            const hipError_t e = hipMalloc((void **)&pw, (size_t)waves_needed * 16 * sizeof(unsigned long long));
+            if (e != hipSuccess) return e;
+            pw_cap = waves_needed;
+        }
+        const hipError_t e = hipMemsetAsync(pw, 0, (size_t)waves_needed * 16 * sizeof(unsigned long long), stream);
+        if (e != hipSuccess) return e;
+        a.prof_waves = pw;
+    }
     a.nB = capacity;
     a.chk = nullptr;
     static int32_t *chk = nullptr;                // RMPC_GROUP_CHECK=1: bounds-check flags
@@ -778,6 +824,26 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
     else if (bs == 1 && N == 10) hipLaunchKernelGGL((mpc_group_kernel<10, 1, 16>), g, blk, lds, stream, a);
     else if (bs == 1 && N == 6) hipLaunchKernelGGL((mpc_group_kernel<6, 1, 16>), g, blk, lds, stream, a);
     else hipLaunchKernelGGL((mpc_group_kernel<6, 2, 16>), g, blk, lds, stream, a);
+    if (a.prof_waves) {           // the slowest waves' phase breakdown (diagnostics)
+        const int64_t n = waves_needed;
+        unsigned long long *h = (unsigned long long *)malloc((size_t)n * 16 * sizeof(unsigned long long));
+        hipError_t e = hipMemcpyAsync(h, a.prof_waves, (size_t)n * 16 * sizeof(unsigned long long),
+                                      hipMemcpyDeviceToHost, stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream);
+        for (int rank = 0; rank < 3 && e == hipSuccess; rank++) {
+            int64_t best = -1;
+            for (int64_t w = 0; w < n; w++)
+                if (h[w * 16 + 10] && (best < 0 || h[w * 16 + 10] > h[best * 16 + 10])) best = w;
+            if (best < 0) break;
+            const unsigned long long *r = h + best * 16;
+            fprintf(stderr, "[group wave %lld] total %llu | setup %llu pn-pre %llu weights %llu back %llu fwd %llu rows %llu "
+                    "out %llu upd %llu ls %llu | loop-its %llu\n", (long long)best, r[10], r[0], r[1], r[2], r[3], r[4],
+                    r[5], r[6], r[7], r[8], r[9]);
+            h[best * 16 + 10] = 0;
+        }
+        free(h);
+        if (e != hipSuccess) return e;
+    }
     if (a.chk) {
         int32_t h = 0;
         hipError_t e = hipMemcpyAsync(&h, a.chk, sizeof(h), hipMemcpyDeviceToHost, stream);
