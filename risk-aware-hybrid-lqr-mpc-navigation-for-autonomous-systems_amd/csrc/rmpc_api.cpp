@@ -75,7 +75,7 @@ struct RmpcCtx {
     DevBuf ws;                 // solver workspace
     DevBuf stage[SB_COUNT];    // staging buffers for host-pointer entry points
     DevBuf idx_lqr, idx_mpc, counts, hyb_status;
-    DevBuf fast_gains, fast_usol, retry, retry2, retry_count, prof, retry_sets;
+    DevBuf fast_gains, retry, retry2, retry_count, prof, retry_sets;
     // closed-loop rollout state (rmpc_rollout_batch)
     DevBuf ro_x, ro_xr, ro_ur, ro_u, ro_step, ro_cache, ro_prev, ro_since, ro_status, ro_used,
         ro_risk, ro_counts, ro_off;
@@ -129,7 +129,6 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     c->counts.release();
     c->hyb_status.release();
     c->fast_gains.release();
-    c->fast_usol.release();
     c->retry.release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -292,7 +291,6 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         const int nb = (p->horizon + bs - 1) / bs;
         const size_t waves = (size_t)((B + RMPC_WAVE_LANES - 1) / RMPC_WAVE_LANES);
         HIP_TRY(c->fast_gains.ensure(waves * nb * 4 * RMPC_WAVE_LANES * sizeof(double2)));
-        HIP_TRY(c->fast_usol.ensure(waves * nb * RMPC_WAVE_LANES * sizeof(double2)));
         HIP_TRY(c->retry.ensure((size_t)B * sizeof(int32_t)));
         HIP_TRY(c->retry_count.ensure(256));
         HIP_TRY(hipMemsetAsync(c->retry_count.p, 0, 64, s));
@@ -307,7 +305,6 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         a.u0 = u0; a.u_seq = u_seq; a.x_pred = x_pred; a.cost = cost;
         a.status = status; a.iters = iters; a.slack_used = slack_used;
         a.gains = (double2 *)c->fast_gains.p;
-        a.usol = (double2 *)c->fast_usol.p;
         a.index = index;
         a.count = count;
         a.retry = (int32_t *)c->retry.p;

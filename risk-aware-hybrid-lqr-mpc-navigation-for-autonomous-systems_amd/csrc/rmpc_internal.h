@@ -48,7 +48,7 @@ struct MpcFastArgs {
     double *u0, *u_seq, *x_pred, *cost;
     int32_t *status, *iters;
     uint8_t *slack_used;
-    double2 *gains, *usol;           // per-wave tiles
+    double2 *gains;                  // per-wave gain tiles
     const int32_t *index, *count;    // optional robot index list (device-side length)
     int32_t *retry, *retry_count;    // robots handed to the next stage
     int pdas_cap;                    // PDAS solves before a robot is handed on

@@ -4,19 +4,20 @@
 // generic kernel in rmpc_mpc.hip, specialised on the horizon N and block size BS so that
 // every per-step quantity of a robot (sin/cos of the unwrapped reference heading, the
 // reference input and position, the hinge flags) lives in VGPRs for the whole solve.
-// Only the block gains (written by the backward sweep, read by the forward sweep) and the
-// block inputs go through a per-wave tile in memory as coalesced 16-byte-per-lane rows,
-// with the forward sweep prefetching PF blocks ahead.  Obstacle rows are recomputed from
-// registers on every pass instead of being streamed.
+// Only the block gains (written by the backward sweep, read by the forward sweep) go
+// through a per-wave tile in memory as coalesced 16-byte-per-lane rows, with the forward
+// sweep prefetching PF blocks ahead; the certified inputs are re-derived from the last
+// gains at output.  Obstacle rows are recomputed from registers on every pass instead of
+// being streamed; the backward sweep skips a row no lane of the wave has active.
 //
 // Templated on the arithmetic type T: double for the fp64 configurations; float for fp32
 // requests (BASELINE config 4: N=30, 8 obstacles), where the register-resident layout would
 // not fit in fp64 at that horizon.  Inputs and outputs stay fp64 in both.
 //
 // One wave per workgroup, one lane per robot.  A robot that is not certified within the
-// PDAS phase (cycling, ~1e-4 of instances) or has non-finite data is appended to a retry
-// list that the generic kernel (projected-Newton phase, fallback law) consumes next on
-// the same stream -- restarting from scratch, so results equal the generic path's.
+// PDAS cap (or has non-finite data) is appended to a retry list, with its active sets, that
+// the lane-group tail (rmpc_mpc_group.hip) continues from; the generic kernel takes what is
+// left (fallback law).
 #include "rmpc_device.h"
 #include "rmpc_internal.h"
 #include "rmpc_riccati.h"
@@ -87,31 +88,6 @@ template <> struct GainTile<float> {
     }
 };
 
-// The block inputs (2 values per block): one 16-byte row in fp64, one 8-byte row in fp32
-template <typename T> struct UsolTile;
-template <> struct UsolTile<double> {
-    WaveRows<16> w;
-    __device__ __forceinline__ UsolTile(void *base, int nb, int lane) : w(base, nb, lane) {}
-    __device__ __forceinline__ void st(int j, double u0, double u1) const {
-        w.st16(j, __builtin_bit_cast(u4v, make_double2(u0, u1)));
-    }
-    __device__ __forceinline__ void ld(int j, double &u0, double &u1) const {
-        const double2 v = __builtin_bit_cast(double2, w.ld16(j));
-        u0 = v.x; u1 = v.y;
-    }
-};
-template <> struct UsolTile<float> {
-    WaveRows<8> w;
-    __device__ __forceinline__ UsolTile(void *base, int nb, int lane) : w(base, nb, lane) {}
-    __device__ __forceinline__ void st(int j, float u0, float u1) const {
-        w.st8(j, __builtin_bit_cast(u2v, make_float2(u0, u1)));
-    }
-    __device__ __forceinline__ void ld(int j, float &u0, float &u1) const {
-        const float2 v = __builtin_bit_cast(float2, w.ld8(j));
-        u0 = v.x; u1 = v.y;
-    }
-};
-
 // Active-set flags packed into few VGPRs (the kernel runs at the register limit; the
 // sweeps are fully unrolled, so every index is a compile-time constant and a get/set is one
 // or two shift/mask instructions).  Hinge rows: 16 bits per step (bit o); box states:
@@ -170,9 +146,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     const T vmax = (T)p.v_max, omax = (T)p.omega_max;
     const double *xr = a.x_refs + ref_row0(a.prm.ref_off, b, a.ref_rows) * 3;
     const double *ur = a.u_refs + ref_row0(a.prm.ref_off, b, a.uref_rows) * 2;
-    // per-wave tiles (sized for fp64; fp32 uses half)
+    // per-wave gain tile (sized for fp64; fp32 uses half)
     const GainTile<T> gt(a.gains + (size_t)blockIdx.x * NB * 4 * RMPC_WAVE, NB, lane);
-    const UsolTile<T> ut(a.usol + (size_t)blockIdx.x * NB * RMPC_WAVE, NB, lane);
 
     // ---- setup: np.unwrap'd reference heading, linearisation data (mpc_controller.py:391-428)
     // sin/cos of the heading and the reference speed stay in VGPRs; the reference position
@@ -363,9 +338,6 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             const int ns0 = box_rule_bf(bf0, e0, lo0, hi0, eps_b), ns1 = box_rule_bf(bf1, e1, lo1, hi1, eps_b);
             changed |= (int)(ns0 != bf0 || ns1 != bf1);
             Bf.set(j, (uint32_t)(ns0 | (ns1 << 2)));
-#ifdef RMPC_FAST_USOL
-            ut.st(j, u0v, u1v);
-#endif
 #pragma unroll
             for (int k = k0; k < k1; k++) {
                 J += Q0 * x0 * x0 + Q1 * x1 * x1 + Q2 * x2 * x2;
@@ -453,9 +425,6 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         T du0, du1;
         const int k0 = j * BS;
         const int k1 = (k0 + BS < N) ? k0 + BS : N;
-#ifdef RMPC_FAST_USOL
-        ut.ld(j, du0, du1);
-#else
         {   // the certified inputs, re-derived from the last backward sweep's gains along the
             // same trajectory (no per-iteration input tile)
             T g[8];
@@ -475,7 +444,6 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             du0 = bf0 == 0 ? e0 : (bf0 == 1 ? lo0 : hi0);
             du1 = bf1 == 0 ? e1 : (bf1 == 1 ? lo1 : hi1);
         }
-#endif
 #pragma unroll
         for (int k = k0; k < k1; k++) {
             double v0 = F64 ? (double)(du0 + V0[k]) : (double)du0 + ur[2 * k];

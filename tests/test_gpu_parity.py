@@ -328,6 +328,34 @@ def test_mpc_closed_loop_drop_in(rm):
     np.testing.assert_allclose(np.array(cts), ct_o, atol=1e-8, rtol=0)
 
 
+def test_mpc_closed_loop_drop_in_hard_constraints(rm):
+    """The same closed loop with use_soft_constraints=False through the drop-in class: each
+    solve (optimal, or infeasible -> fallback law with the step count held) matches the
+    oracle controller fed the same states.  Parity unpinned by reference artefacts."""
+    g = figure8.Figure8(2.0, 0.5, 0.02)
+    g.generate(20.0)
+    kw = dict(horizon=6, Q_diag=[15, 15, 50], R_diag=[.1, .1], P_diag=[30, 30, 40], d_safe=0.3,
+              slack_penalty=5000.0, dt=0.02, v_max=2.0, omega_max=3.0, solver="OSQP", block_size=2)
+    c = rm.MPCController(**kw)
+    oc = ompc.MPCController(6, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02,
+                            "OSQP", 2)
+    obs = [rm.Obstacle(*o) for o in ompc.default_obstacles()]
+    x = g.reference_at_index(0)[0].copy()
+    statuses = set()
+    for k in range(0, 300, 5):
+        xr, ur = g.segment(k, 7)
+        sol = c.solve_with_ltv(x, xr, ur, obs, use_soft_constraints=False)
+        ref = oc.solve_with_ltv(x, xr, ur, ompc.default_obstacles(), use_soft_constraints=False)
+        statuses.add(ref.status)
+        assert sol.status == ref.status, (k, sol.status, ref.status)
+        np.testing.assert_allclose(sol.control_sequence, ref.control_sequence, atol=1e-9, rtol=0)
+        assert not sol.slack_used
+        assert c._step_count == oc._step_count
+        for _ in range(5):
+            x = oplant.simulate_step(x, sol.optimal_control, 0.02, 2.0, 3.0)
+    assert "optimal" in statuses
+
+
 # ------------------------------------------------------------------------------------ misc
 def test_risk_matches_reference(rm, golden):
     d = golden("risk.npz")
