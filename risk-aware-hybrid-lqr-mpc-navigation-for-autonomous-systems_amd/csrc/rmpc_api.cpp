@@ -339,13 +339,15 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         const bool use_dense = tail && !strcmp(tail, "dense");
         // tail PDAS cap before projected Newton (sweeps: 4 at N <= 20, 6 beyond -- config 4)
         const int tail_cap = getenv("RMPC_DENSE_CAP") ? atoi(getenv("RMPC_DENSE_CAP")) : (p->horizon <= 20 ? 4 : 6);
+        // fp32 requests get the fp32 lane-group tail (RMPC_TAIL64=1: the fp64 one)
+        const bool tail32 = f32 && !getenv("RMPC_TAIL64") && rmpc_mpc_group_supported(p->horizon, bs, n_obs, true);
         if (!use_dense && rmpc_mpc_group_supported(p->horizon, bs, n_obs) && !getenv("RMPC_DISABLE_DENSE")) {
             HIP_TRY(c->retry2.ensure((size_t)B * sizeof(int32_t)));
             int32_t *cnt2 = (int32_t *)c->retry_count.p + 8;
             HIP_TRY(rmpc_launch_mpc_group(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs, uref_rows,
                                           obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
                                           iters, left, left_n, (int32_t *)c->retry2.p, cnt2, tail_cap,
-                                          a.retry_sets, s, pc));
+                                          a.retry_sets, s, pc, tail32));
             if (prof) {
                 unsigned long long h[64];
                 int32_t cn[16];

@@ -69,7 +69,7 @@ hipError_t rmpc_launch_mpc_dense_f64(const MpcDevParams &prm, int N, int bs, int
                                      const uint32_t *warm, hipStream_t stream,
                                      unsigned long long *prof = nullptr);
 hipError_t rmpc_launch_mpc_fast(const MpcFastArgs &a, int N, int bs, int prec, hipStream_t stream);
-bool rmpc_mpc_group_supported(int N, int bs, int no);
+bool rmpc_mpc_group_supported(int N, int bs, int no, bool f32 = false);
 hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no, int64_t capacity,
                                  const double *x0, const double *x_refs, int ref_rows,
                                  const double *u_refs, int uref_rows, const double *obstacles,
@@ -77,7 +77,7 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
                                  double *cost, int32_t *status, uint8_t *slack_used, int32_t *iters,
                                  const int32_t *index, const int32_t *count, int32_t *retry,
                                  int32_t *retry_count, int pdas_cap, const uint32_t *warm,
-                                 hipStream_t stream, unsigned long long *prof = nullptr);
+                                 hipStream_t stream, unsigned long long *prof = nullptr, bool f32 = false);
 
 hipError_t rmpc_launch_mpc_f64(const MpcDevParams &prm, const MpcLayout &L, int64_t B,
                                const double *x0, const double *x_refs, int ref_rows,

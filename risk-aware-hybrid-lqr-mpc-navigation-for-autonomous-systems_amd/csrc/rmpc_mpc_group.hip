@@ -67,11 +67,11 @@ __device__ __forceinline__ void group_retry(const GroupArgs &a, int64_t b) {
         }                                                                             \
     } while (0)
 
-// One robot's LDS record (doubles).  Every region but the hinge rows has a compile-time
+// One robot's LDS record (elements of the arithmetic type T).  Every region but the hinge rows has a compile-time
 // offset, so the optimiser can prove the recursions' stores (gains, trajectory) disjoint
 // from their loads (step data) and issue the loads ahead; per-step and per-block data are
 // packed 16-byte aligned records (ds_read_b128).
-template <int N, int NB>
+template <int N, int NB, typename T>
 struct GRec {
     static constexpr int STEP = 0;                 // [N][12]: a0 a1 b0 b1 us0 us1 q00 q01 q11 qv0 qv1 -
     static constexpr int BLK = STEP + 12 * N;      // [NB][12]: lo0 hi0 lo1 hi1 G0..G7
@@ -84,10 +84,11 @@ struct GRec {
     static constexpr int ZF = FR + 2 * N;          // certified inputs, kept for the final write [2NB]
     static constexpr int XF = ZF + 2 * NB;         // certified trajectory [N+1][3]
     static constexpr int INT = XF + 3 * (N + 1);   // uint32: HF [N], BF [NB], NHF [N], NBF [NB]
-    static constexpr int HR = INT + (N + NB + 1) / 2 * 2;   // hinge rows [3][no][N] (runtime no)
+    static constexpr int INTN = ((2 * N + 2 * NB) * 4 + (int)sizeof(T) - 1) / (int)sizeof(T);
+    static constexpr int HR = INT + (INTN + 1) / 2 * 2;     // hinge rows [3][no][N] (runtime no)
     __host__ __device__ static int size(int no) {
         const int o = HR + 3 * no * N;
-        return o + (8 - o % 32 + 32) % 32;         // stride = 8 (mod 32) doubles: the groups'
+        return o + (8 - o % 32 + 32) % 32;         // stride = 8 (mod 32) elements: the groups'
     }                                              // broadcast reads fall on different banks
 };
 
@@ -98,15 +99,15 @@ __device__ __forceinline__ bool gany(bool v, int grp) {
     return ((m >> (grp * G)) & ((1ull << G) - 1)) != 0;
 }
 
-template <int G>
-__device__ __forceinline__ double gsum(double v) {
+template <int G, typename V>
+__device__ __forceinline__ V gsum(V v) {
 #pragma unroll
     for (int off = G / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
     return v;
 }
 
-template <int G>
-__device__ __forceinline__ double gmaxv(double v) {
+template <int G, typename V>
+__device__ __forceinline__ V gmaxv(V v) {
 #pragma unroll
     for (int off = G / 2; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
     return v;
@@ -121,17 +122,17 @@ enum { PH_PDAS = 0, PH_PN = 1, PH_DONE = 2, PH_IDLE = 3 };
 // Stores that only some groups may make (GSTM) select a private junk slot instead.
 __shared__ double grp_junk[64];
 
-template <int N, int BS, int G>
-__device__ __forceinline__ void group_solve(const GroupArgs &a, double *const base0,
+template <int N, int BS, int G, typename T>
+__device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
                                             int t, bool have, int gl, int grp) {
     constexpr int NB = (N + BS - 1) / BS;
     constexpr int KPL = (N + G - 1) / G;          // steps per lane
     const MpcDevParams &p = a.prm;
     const int no = a.no;
-    const double dt = p.dt, rho = p.rho;
-    const double Q0 = p.Q[0], Q1 = p.Q[1], Q2 = p.Q[2], R0 = p.R[0], R1 = p.R[1];
-    const double P0 = p.P[0], P1 = p.P[1], P2 = p.P[2];
-    const double eps_h = SetTol<double>::hinge, eps_b = SetTol<double>::box;
+    const T dt = p.dt, rho = p.rho;
+    const T Q0 = p.Q[0], Q1 = p.Q[1], Q2 = p.Q[2], R0 = p.R[0], R1 = p.R[1];
+    const T P0 = p.P[0], P1 = p.P[1], P2 = p.P[2];
+    const T eps_h = SetTol<T>::hinge, eps_b = SetTol<T>::box;
     int64_t b = have ? (int64_t)a.index[t] : 0;
     if (a.chk && have && (b < 0 || b >= a.nB)) { atomicOr(a.chk, 1); b = 0; have = false; }
     const double *xr = a.x_refs + ref_row0(a.prm.ref_off, b, a.ref_rows) * 3;
@@ -143,8 +144,8 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
 
     // LDS views, re-derived from an opaque offset before each use so that the optimiser
     // cannot hoist the (loop-invariant) per-step data out of the iteration loop
-    double *base = base0;
-    double *const junk = grp_junk + threadIdx.x;
+    T *base = base0;
+    T *const junk = reinterpret_cast<T *>(grp_junk) + threadIdx.x;
 // GST: every lane of the group stores its (bitwise identical) copy -- no address select;
 // GSTM: masked per group through the junk slot (groups whose values are not meaningful)
 #define GST(ref, v) ((ref) = (v))
@@ -154,7 +155,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
         asm volatile("" : "+v"(o));
         base = base0 + o;
     };
-    using RC = GRec<N, NB>;
+    using RC = GRec<N, NB, T>;
 #define STG(f, k) base[RC::STEP + 12 * (k) + (f)]
 #define WQ(k, f) base[RC::STEP + 12 * (k) + 6 + (f)]
 #define BND(f, j) base[RC::BLK + 12 * (j) + (f)]
@@ -203,12 +204,14 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
             STG(3, k) = sn * dt;
             STG(4, k) = v;
             STG(5, k) = w;
-            const double px = xr[3 * k], py = xr[3 * k + 1];
+            const T px = (T)xr[3 * k], py = (T)xr[3 * k + 1];
             fin = fin && isfinite(sn + cs + v + w + px + py);
             for (int o = 0; o < no; o++) {
-                double n0, n1, hb;
-                if (!hinge_row_fast(px, py, a.obs[3 * o], a.obs[3 * o + 1], p.d_safe + a.obs[3 * o + 2], n0, n1, hb)) {
-                    n0 = 0; n1 = 0; hb = -1e300;                             // row not kept
+                T n0, n1, hb;
+                // (in T, from the same rounded inputs as the lane-per-robot kernel's rows)
+                if (!hinge_row_fast(px, py, (T)a.obs[3 * o], (T)a.obs[3 * o + 1], (T)(p.d_safe + a.obs[3 * o + 2]),
+                                    n0, n1, hb)) {
+                    n0 = 0; n1 = 0; hb = (T)(sizeof(T) == 8 ? -1e300 : -1e30);   // row not kept
                 }
                 HN0(o, k) = n0;
                 HN1(o, k) = n1;
@@ -228,7 +231,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
     }
     const double *x0p = a.x0 + 3 * b;
     const double x0a = th0 + wrap_pi(x0p[2] - th0);                        // :397-401
-    const double d0 = x0p[0] - xr[0], d1 = x0p[1] - xr[1], d2 = x0a - th0;
+    const T d0 = (T)(x0p[0] - xr[0]), d1 = (T)(x0p[1] - xr[1]), d2 = (T)(x0a - th0);
     fin = fin && isfinite(d0 + d1 + d2);
     int it0 = 0;                      // iterations of the previous stage (reported in iters)
     {
@@ -252,21 +255,21 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
     // trajectory under the inputs Z (ZC / ZZ / ZT) -> XS, full objective (constants included,
     // as the fast kernel's J), and whether any hinge residual exceeds 1e-6 (slack_used, :485)
     // full objective of the inputs at zoff along the trajectory in XS (lane-parallel)
-    auto cost = [&](int zoff, int &used) __attribute__((always_inline)) -> double {
+    auto cost = [&](int zoff, int &used) __attribute__((always_inline)) -> T {
         refresh();
-        double jl = 0.0;
+        T jl = 0.0;
         int u = 0;
         for (int k = gl; k <= N; k += G) {
-            const double y0 = XS(k, 0), y1 = XS(k, 1), y2 = XS(k, 2);
+            const T y0 = XS(k, 0), y1 = XS(k, 1), y2 = XS(k, 2);
             if (k == N) {
                 jl += P0 * y0 * y0 + P1 * y1 * y1 + P2 * y2 * y2;
             } else {
                 jl += Q0 * y0 * y0 + Q1 * y1 * y1 + Q2 * y2 * y2;
                 const int j = k / BS;
-                const double uu0 = base[zoff + 2 * j] + STG(4, k), uu1 = base[zoff + 2 * j + 1] + STG(5, k);
+                const T uu0 = base[zoff + 2 * j] + STG(4, k), uu1 = base[zoff + 2 * j + 1] + STG(5, k);
                 jl += R0 * uu0 * uu0 + R1 * uu1 * uu1;
                 for (int o = 0; o < no; o++) {
-                    const double r = HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1;
+                    const T r = HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1;
                     if (r > 0) jl += rho * r * r;
                     u |= (r > 1e-6);
                 }
@@ -276,11 +279,11 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
         return gsum<G>(jl);
     };
 
-    auto objective = [&](int zoff, bool m, int &used) __attribute__((always_inline)) -> double {
+    auto objective = [&](int zoff, bool m, int &used) __attribute__((always_inline)) -> T {
         refresh();
-        double x0 = d0, x1 = d1, x2 = d2;
+        T x0 = d0, x1 = d1, x2 = d2;
         // per step: inputs of its block + linearisation, step k+1's loaded while k computes
-        double nx[6];
+        T nx[6];
         auto ldo = [&](int k) __attribute__((always_inline)) {
             nx[0] = base[zoff + 2 * (k / BS)];
             nx[1] = base[zoff + 2 * (k / BS) + 1];
@@ -290,15 +293,15 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
         ldo(0);
 #pragma unroll
         for (int k = 0; k < N; k++) {
-            double c[6];
+            T c[6];
 #pragma unroll
             for (int f = 0; f < 6; f++) c[f] = nx[f];
             if (k + 1 < N) ldo(k + 1);
             __builtin_amdgcn_sched_barrier(0);
             GSTM(XS(k, 0), x0, m); GSTM(XS(k, 1), x1, m); GSTM(XS(k, 2), x2, m);
-            const double n0 = x0 + c[2] * x2 + c[4] * c[0];
-            const double n1 = x1 + c[3] * x2 + c[5] * c[0];
-            const double n2 = x2 + dt * c[1];
+            const T n0 = x0 + c[2] * x2 + c[4] * c[0];
+            const T n1 = x1 + c[3] * x2 + c[5] * c[0];
+            const T n2 = x2 + dt * c[1];
             x0 = n0; x1 = n1; x2 = n2;
         }
         GSTM(XS(N, 0), x0, m); GSTM(XS(N, 1), x1, m); GSTM(XS(N, 2), x2, m);
@@ -313,12 +316,12 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
         refresh();
         // per-step stage weights from the active rows (lane-parallel over steps)
         for (int k = gl; k < N; k += G) {
-            double q00 = Q0, q01 = 0.0, q11 = Q1, qv0 = -Q0 * 0.0, qv1 = -Q1 * 0.0;
+            T q00 = Q0, q01 = 0.0, q11 = Q1, qv0 = -Q0 * (T)0, qv1 = -Q1 * (T)0;
             const uint32_t h = HF(k);
             if (k > 0 && h) {
                 for (int o = 0; o < no; o++) {
                     if (!((h >> o) & 1u)) continue;
-                    const double n0 = HN0(o, k), n1 = HN1(o, k), hb = HB(o, k);
+                    const T n0 = HN0(o, k), n1 = HN1(o, k), hb = HB(o, k);
                     q00 += rho * n0 * n0;
                     q01 += rho * n0 * n1;
                     q11 += rho * n1 * n1;
@@ -332,13 +335,13 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
         GPROF(2);
         refresh();
         // backward block Riccati sweep (uniform within the group)
-        RicV<double> V;
+        RicV<T> V;
         V.P00 = P0; V.P01 = 0; V.P02 = 0; V.P11 = P1; V.P12 = 0; V.P22 = P2;
         V.p0 = -P0 * 0.0; V.p1 = -P1 * 0.0; V.p2 = -P2 * 0.0;
         if constexpr (BS == 1) {
             // single-step blocks, software-pipelined: step j-1's record is loaded while step j
             // computes (the scheduler does not hoist LDS loads across unrolled steps itself)
-            double nx[16];
+            T nx[16];
             uint32_t nbf = 0;
             auto ld = [&](int j) __attribute__((always_inline)) {
 #pragma unroll
@@ -350,15 +353,15 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
             ld(NB - 1);
 #pragma unroll
             for (int j = NB - 1; j >= 0; j--) {
-                double c[16];
+                T c[16];
 #pragma unroll
                 for (int f = 0; f < 16; f++) c[f] = nx[f];
                 const uint32_t bfj = nbf;
                 if (j > 0) ld(j - 1);
                 __builtin_amdgcn_sched_barrier(0);
                 const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
-                double Gv[8];
-                V = ric_step1_bf(V, c[0], c[1], c[2], c[3], dt, c[6], c[7], c[8], Q2, c[9], c[10], -Q2 * 0.0, R0, R1,
+                T Gv[8];
+                V = ric_step1_bf(V, c[0], c[1], c[2], c[3], dt, c[6], c[7], c[8], Q2, c[9], c[10], -Q2 * (T)0, R0, R1,
                                  R0 * c[4], R1 * c[5], bf0, bf1, bf0 == 1 ? c[12] : c[13], bf1 == 1 ? c[14] : c[15], Gv);
 #pragma unroll
                 for (int q = 0; q < 8; q++) GST(GN(j, q), Gv[q]);
@@ -369,12 +372,12 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
                 const int k0 = j * BS, k1 = (k0 + BS < N) ? k0 + BS : N;
                 const uint32_t bfj = BF(j);
                 const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
-                double Gv[8];
-                RicW<double> W = ric_open(V);
+                T Gv[8];
+                RicW<T> W = ric_open(V);
 #pragma unroll
                 for (int k = k1 - 1; k >= k0; k--) {
                     ric_step(W, STG(0, k), STG(1, k), STG(2, k), STG(3, k), dt, WQ(k, 0), WQ(k, 1), WQ(k, 2), Q2,
-                             WQ(k, 3), WQ(k, 4), -Q2 * 0.0, R0, R1, R0 * STG(4, k), R1 * STG(5, k));
+                             WQ(k, 3), WQ(k, 4), -Q2 * (T)0, R0, R1, R0 * STG(4, k), R1 * STG(5, k));
                 }
                 V = ric_block_bf(W, bf0, bf1, bf0 == 1 ? BND(0, j) : BND(1, j), bf1 == 1 ? BND(2, j) : BND(3, j), Gv);
 #pragma unroll
@@ -387,32 +390,32 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
         // forward sweep: inputs (free: gains; fixed: bound), box rule on the value (free) or
         // the multiplier (fixed), trajectory
         bool bchg = false;
-        double x0 = d0, x1 = d1, x2 = d2;
+        T x0 = d0, x1 = d1, x2 = d2;
         // block record (bounds + gains) and step data of block j+1 loaded while j computes
-        double nx[16];
+        T nx[16];
         uint32_t nbf = 0;
         auto ldf = [&](int j) __attribute__((always_inline)) {
 #pragma unroll
             for (int f = 0; f < 12; f++) nx[f] = base[RC::BLK + 12 * j + f];
 #pragma unroll
-            for (int f = 0; f < 4; f++) nx[12 + f] = BS == 1 ? base[RC::STEP + 12 * j + f] : 0.0;
+            for (int f = 0; f < 4; f++) nx[12 + f] = BS == 1 ? base[RC::STEP + 12 * j + f] : (T)0;
             nbf = BF(j);
         };
         ldf(0);
 #pragma unroll
         for (int j = 0; j < NB; j++) {
-            double c[16];
+            T c[16];
 #pragma unroll
             for (int f = 0; f < 16; f++) c[f] = nx[f];
             const uint32_t bfj = nbf;
             if (j + 1 < NB) ldf(j + 1);
             __builtin_amdgcn_sched_barrier(0);
-            const double lo0 = c[0], hi0 = c[1], lo1 = c[2], hi1 = c[3];
-            const double e0 = c[4] * x0 + c[5] * x1 + c[6] * x2 + c[10];
-            const double e1 = c[7] * x0 + c[8] * x1 + c[9] * x2 + c[11];
+            const T lo0 = c[0], hi0 = c[1], lo1 = c[2], hi1 = c[3];
+            const T e0 = c[4] * x0 + c[5] * x1 + c[6] * x2 + c[10];
+            const T e1 = c[7] * x0 + c[8] * x1 + c[9] * x2 + c[11];
             const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
-            const double u0v = bf0 == 0 ? e0 : (bf0 == 1 ? lo0 : hi0);
-            const double u1v = bf1 == 0 ? e1 : (bf1 == 1 ? lo1 : hi1);
+            const T u0v = bf0 == 0 ? e0 : (bf0 == 1 ? lo0 : hi0);
+            const T u1v = bf1 == 0 ? e1 : (bf1 == 1 ? lo1 : hi1);
             const int ns0 = box_rule_bf(bf0, e0, lo0, hi0, eps_b), ns1 = box_rule_bf(bf1, e1, lo1, hi1, eps_b);
             bchg = bchg || ns0 != bf0 || ns1 != bf1;
             NBF(j) = (uint32_t)(ns0 | (ns1 << 2));
@@ -421,11 +424,11 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
 #pragma unroll
             for (int k = j * BS; k < (j + 1) * BS && k < N; k++) {
                 GST(XS(k, 0), x0); GST(XS(k, 1), x1); GST(XS(k, 2), x2);
-                const double sa0 = BS == 1 ? c[12] : STG(0, k), sa1 = BS == 1 ? c[13] : STG(1, k);
-                const double sb0 = BS == 1 ? c[14] : STG(2, k), sb1 = BS == 1 ? c[15] : STG(3, k);
-                const double n0 = x0 + sa0 * x2 + sb0 * u0v;
-                const double n1 = x1 + sa1 * x2 + sb1 * u0v;
-                const double n2 = x2 + dt * u1v;
+                const T sa0 = BS == 1 ? c[12] : STG(0, k), sa1 = BS == 1 ? c[13] : STG(1, k);
+                const T sb0 = BS == 1 ? c[14] : STG(2, k), sb1 = BS == 1 ? c[15] : STG(3, k);
+                const T n0 = x0 + sa0 * x2 + sb0 * u0v;
+                const T n1 = x1 + sa1 * x2 + sb1 * u0v;
+                const T n2 = x2 + dt * u1v;
                 x0 = n0; x1 = n1; x2 = n2;
             }
         }
@@ -439,9 +442,9 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
             const uint32_t h = HF(k);
             uint32_t nh = h;
             if (k > 0) {
-                const double y0 = XS(k, 0), y1 = XS(k, 1);
+                const T y0 = XS(k, 0), y1 = XS(k, 1);
                 for (int o = 0; o < no; o++) {
-                    const double r = HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1;
+                    const T r = HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1;
                     const uint32_t act = (h >> o) & 1u;
                     const uint32_t na = act ? (r > -eps_h) : (r > eps_h);
                     nh ^= (na ^ act) << o;
@@ -461,11 +464,11 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
     auto gradient = [&](bool m) __attribute__((always_inline)) {
         refresh();
         for (int k = gl; k < N; k += G) {
-            double f0 = 0.0, f1 = 0.0;
+            T f0 = 0.0, f1 = 0.0;
             if (k > 0) {
-                const double y0 = XS(k, 0), y1 = XS(k, 1);
+                const T y0 = XS(k, 0), y1 = XS(k, 1);
                 for (int o = 0; o < no; o++) {
-                    const double r = HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1;
+                    const T r = HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1;
                     if (r > 0) {
                         f0 -= 2 * rho * r * HN0(o, k);
                         f1 -= 2 * rho * r * HN1(o, k);
@@ -476,18 +479,18 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
         }
         __syncthreads();
         refresh();
-        double l0 = 2 * P0 * XS(N, 0), l1 = 2 * P1 * XS(N, 1), l2 = 2 * P2 * XS(N, 2);
+        T l0 = 2 * P0 * XS(N, 0), l1 = 2 * P1 * XS(N, 1), l2 = 2 * P2 * XS(N, 2);
 #pragma unroll
         for (int j = NB - 1; j >= 0; j--) {
-            double g0 = 0.0, g1 = 0.0;
-            const double z0 = ZZ(2 * j), z1 = ZZ(2 * j + 1);
+            T g0 = 0.0, g1 = 0.0;
+            const T z0 = ZZ(2 * j), z1 = ZZ(2 * j + 1);
 #pragma unroll
             for (int k = ((j + 1) * BS < N ? (j + 1) * BS : N) - 1; k >= j * BS; k--) {
                 g0 += STG(2, k) * l0 + STG(3, k) * l1 + 2 * R0 * (z0 + STG(4, k));
                 g1 += dt * l2 + 2 * R1 * (z1 + STG(5, k));
-                const double m0 = 2 * Q0 * XS(k, 0) + l0 + (k > 0 ? FR(0, k) : 0.0);
-                const double m1 = 2 * Q1 * XS(k, 1) + l1 + (k > 0 ? FR(1, k) : 0.0);
-                const double m2 = 2 * Q2 * XS(k, 2) + STG(0, k) * l0 + STG(1, k) * l1 + l2;
+                const T m0 = 2 * Q0 * XS(k, 0) + l0 + (k > 0 ? FR(0, k) : (T)0);
+                const T m1 = 2 * Q1 * XS(k, 1) + l1 + (k > 0 ? FR(1, k) : (T)0);
+                const T m2 = 2 * Q2 * XS(k, 2) + STG(0, k) * l0 + STG(1, k) * l1 + l2;
                 l0 = m0; l1 = m1; l2 = m2;
             }
             GSTM(GR(2 * j), g0, m); GSTM(GR(2 * j + 1), g1, m);
@@ -500,7 +503,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
     double J_out = 0.0;
     int used_out = 0, it_out = 0;
     int it = 0, cyc = 0;
-    double F = 0.0;
+    T F = 0.0;
     uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
     const int max_iter = p.max_iter;
     while (__any(phase <= PH_PN)) {
@@ -511,19 +514,19 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
             // r > 0 -- the sets of this solve (rmpc_mpc_dense.hip phase 2)
             gradient(pn);
             refresh();
-            double wl = 0.0;
+            T wl = 0.0;
             for (int i = gl; i < 2 * NB; i += G) {
                 const int j = i >> 1, c = i & 1;
-                const double lo = BND(2 * c, j), hi = BND(2 * c + 1, j), z = ZZ(i);
+                const T lo = BND(2 * c, j), hi = BND(2 * c + 1, j), z = ZZ(i);
                 wl = fmax(wl, fabs(z - clampv(z - GR(i), lo, hi)));
             }
-            const double eps = fmin(1e-6, gmaxv<G>(wl));
+            const T eps = fmin(SetTol<T>::pn, gmaxv<G>(wl));
             if (pn) {
                 for (int j = gl; j < NB; j += G) {
                     uint32_t w = 0;
 #pragma unroll
                     for (int c = 0; c < 2; c++) {
-                        const double lo = BND(2 * c, j), hi = BND(2 * c + 1, j), z = ZZ(2 * j + c), g = GR(2 * j + c);
+                        const T lo = BND(2 * c, j), hi = BND(2 * c + 1, j), z = ZZ(2 * j + c), g = GR(2 * j + c);
                         const uint32_t s = (z <= lo + eps && g > 0) ? 1u : ((z >= hi - eps && g < 0) ? 2u : 0u);
                         w |= s << (2 * c);
                     }
@@ -532,7 +535,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
                 for (int k = gl; k < N; k += G) {
                     uint32_t nh = 0;
                     if (k > 0) {
-                        const double y0 = XS(k, 0), y1 = XS(k, 1);
+                        const T y0 = XS(k, 0), y1 = XS(k, 1);
                         for (int o = 0; o < no; o++)
                             if (HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1 > 0) nh |= 1u << o;
                     }
@@ -550,7 +553,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
             // certifying solve's forward sweep), and a copy of inputs + trajectory kept for
             // the single output write after the loop (later sweeps overwrite ZC / XS)
             int used = 0;
-            const double J = cost(RC::ZC, used);
+            const T J = cost(RC::ZC, used);
             refresh();
             if (cert && isfinite(J)) {
                 for (int i = gl; i < 2 * NB; i += G) ZF(i) = ZC(i);
@@ -597,7 +600,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
             }
             __syncthreads();
             int u;
-            const double f = objective(RC::ZZ, to_pn, u);
+            const T f = objective(RC::ZZ, to_pn, u);
             if (to_pn) { F = f; phase = PH_PN; }
             __syncthreads();
         }
@@ -606,28 +609,28 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
         bool searching = pn && !cert;
         if (__any(searching)) {
             refresh();
-            double alpha = 1.0;
+            T alpha = 1.0;
             for (int ls = 0; ls < 40 && __any(searching); ls++) {
-                double gd = 0.0;
+                T gd = 0.0;
                 for (int i = gl; i < 2 * NB; i += G) {
                     const int j = i >> 1, c = i & 1;
-                    const double z = ZZ(i);
-                    const double zt = clampv(z + alpha * (ZC(i) - z), BND(2 * c, j), BND(2 * c + 1, j));
+                    const T z = ZZ(i);
+                    const T zt = clampv(z + alpha * (ZC(i) - z), BND(2 * c, j), BND(2 * c + 1, j));
                     if (searching) ZT(i) = zt;
                     gd += GR(i) * (zt - z);
                 }
                 gd = gsum<G>(gd);
                 __syncthreads();
                 int u;
-                const double Ft = objective(RC::ZT, searching, u);
+                const T Ft = objective(RC::ZT, searching, u);
                 refresh();
-                const bool acc = searching && Ft <= F + 1e-4 * gd;
+                const bool acc = searching && Ft <= F + (T)1e-4 * gd;
                 if (acc) {
                     for (int i = gl; i < 2 * NB; i += G) ZZ(i) = ZT(i);
                     F = Ft;
                     searching = false;
                 }
-                alpha *= 0.5;
+                alpha *= (T)0.5;
                 __syncthreads();
             }
             if (searching) fail = true;          // no acceptable step
@@ -649,8 +652,11 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
             const int sc = a.step_count ? a.step_count[b] : 0;
             for (int k = gl; k < N; k += G) {
                 const int j = k / BS;
-                const double v0 = ZF(2 * j) + STG(4, k);
-                double v1 = ZF(2 * j + 1) + STG(5, k);
+                // fp64: u = du + u_ref in the record; fp32: du + the fp64 u_ref (only the
+                // deviation carries fp32 rounding, as in the lane-per-robot kernel)
+                constexpr bool F64 = sizeof(T) == 8;
+                const double v0 = F64 ? (double)(ZF(2 * j) + STG(4, k)) : (double)ZF(2 * j) + ur[2 * k];
+                double v1 = F64 ? (double)(ZF(2 * j + 1) + STG(5, k)) : (double)ZF(2 * j + 1) + ur[2 * k + 1];
                 if (k == 0 && sc < p.ramp_up_steps) {                      // :502-505
                     const double lim = p.omega_max * ((double)(sc + 1) / (double)p.ramp_up_steps);
                     v1 = clampv(v1, -lim, lim);
@@ -667,9 +673,9 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
             if (a.x_pred) {                                                 // :497
                 for (int k = gl; k <= N; k += G) {
                     double *xp = a.x_pred + ((size_t)b * (N + 1) + k) * 3;
-                    xp[0] = XF(k, 0) + xr[3 * k];
-                    xp[1] = XF(k, 1) + xr[3 * k + 1];
-                    xp[2] = XF(k, 2) + xr[3 * k + 2];
+                    xp[0] = (double)XF(k, 0) + xr[3 * k];
+                    xp[1] = (double)XF(k, 1) + xr[3 * k + 1];
+                    xp[2] = (double)XF(k, 2) + xr[3 * k + 2];
                 }
             }
             if (gl == 0) {
@@ -718,31 +724,33 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, double *const ba
 // tail's run time).  A persistent variant that looped over rounds faulted from its second
 // round on (every robot's accesses in bounds, checked with RMPC_GROUP_CHECK), so there is
 // no round loop.
-template <int N, int BS, int G>
+template <int N, int BS, int G, typename T>
 __global__ __launch_bounds__(64, 1) void mpc_group_kernel(GroupArgs a) {
     constexpr int NB = (N + BS - 1) / BS, RPW = 64 / G;
-    extern __shared__ double lds[];
+    extern __shared__ double lds_raw[];
+    T *const lds = reinterpret_cast<T *>(lds_raw);
     const int lane = threadIdx.x, gl = lane % G, grp = lane / G;
-    const int rec = GRec<N, NB>::size(a.no);
+    const int rec = GRec<N, NB, T>::size(a.no);
     const int cnt = *a.count;
     if (a.chk && lane == 0 && blockIdx.x == 0 && (cnt < 0 || cnt > a.nB)) atomicOr(a.chk, 2);
     const int t0 = blockIdx.x * RPW;
     if (t0 >= cnt) return;
     const int t = t0 + grp;
-    group_solve<N, BS, G>(a, lds + grp * rec, t, t < cnt, gl, grp);
+    group_solve<N, BS, G, T>(a, lds + grp * rec, t, t < cnt, gl, grp);
 }
 
 // lanes per robot: 16 (four robots per wave) while the record leaves room for four waves
 // per CU, else 32
 static int group_lanes(int N, int bs) { return N > 20 ? 32 : 16; }
 
-static int group_rec(int N, int bs, int no) {
-    if (bs == 2 && N == 6) return GRec<6, 3>::size(no);
+// record bytes per robot for the arithmetic of `f32`
+static size_t group_rec_bytes(int N, int bs, int no, bool f32) {
+    if (bs == 2 && N == 6) return GRec<6, 3, double>::size(no) * sizeof(double);
     switch (N) {
-        case 6: return GRec<6, 6>::size(no);
-        case 10: return GRec<10, 10>::size(no);
-        case 20: return GRec<20, 20>::size(no);
-        default: return GRec<30, 30>::size(no);
+        case 6: return GRec<6, 6, double>::size(no) * sizeof(double);
+        case 10: return GRec<10, 10, double>::size(no) * sizeof(double);
+        case 20: return GRec<20, 20, double>::size(no) * sizeof(double);
+        default: return GRec<30, 30, double>::size(no) * sizeof(double);
     }
 }
 
@@ -750,10 +758,14 @@ static int group_rec(int N, int bs, int no) {
 
 using namespace rmpc;
 
-bool rmpc_mpc_group_supported(int N, int bs, int no) {
+// The kernel is templated on its arithmetic type, but only the fp64 instances ship: an fp32
+// instance (for the fp32 requests of BASELINE config 4) faulted the GPU in its first parity
+// run, so fp32 requests keep the fp64 tail.
+bool rmpc_mpc_group_supported(int N, int bs, int no, bool f32) {
+    if (f32) return false;
     const bool inst = (bs == 1 && (N == 6 || N == 10 || N == 20 || N == 30)) || (bs == 2 && N == 6);
     if (!inst || no > 16) return false;
-    const size_t lds = (size_t)(64 / group_lanes(N, bs)) * group_rec(N, bs, no) * sizeof(double);
+    const size_t lds = (size_t)(64 / group_lanes(N, bs)) * group_rec_bytes(N, bs, no, f32);
     return lds <= 160 * 1024;
 }
 
@@ -764,9 +776,9 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
                                  double *cost, int32_t *status, uint8_t *slack_used, int32_t *iters,
                                  const int32_t *index, const int32_t *count, int32_t *retry,
                                  int32_t *retry_count, int pdas_cap, const uint32_t *warm,
-                                 hipStream_t stream, unsigned long long *prof) {
+                                 hipStream_t stream, unsigned long long *prof, bool f32) {
     if (capacity <= 0) return hipSuccess;
-    if (!rmpc_mpc_group_supported(N, bs, no)) return hipErrorInvalidValue;
+    if (!rmpc_mpc_group_supported(N, bs, no, f32)) return hipErrorInvalidValue;
     GroupArgs a;
     a.prm = prm;
     a.no = no;
@@ -807,23 +819,23 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
     }
     a.pdas_cap = pdas_cap < RMPC_PDAS_ITERS ? pdas_cap : RMPC_PDAS_ITERS;
     const int G = group_lanes(N, bs), rpw = 64 / G;
-    const size_t lds = (size_t)rpw * group_rec(N, bs, no) * sizeof(double);
+    const size_t lds = (size_t)rpw * group_rec_bytes(N, bs, no, f32);
     const int64_t need = (capacity + rpw - 1) / rpw;
     const dim3 g((unsigned)need), blk(64);
-    const void *fn = (bs == 1 && N == 30)   ? (const void *)mpc_group_kernel<30, 1, 32>
-                     : (bs == 1 && N == 20) ? (const void *)mpc_group_kernel<20, 1, 16>
-                     : (bs == 1 && N == 10) ? (const void *)mpc_group_kernel<10, 1, 16>
-                     : (bs == 1 && N == 6)  ? (const void *)mpc_group_kernel<6, 1, 16>
-                                            : (const void *)mpc_group_kernel<6, 2, 16>;
+    const void *fn = (bs == 1 && N == 30)   ? (const void *)mpc_group_kernel<30, 1, 32, double>
+                     : (bs == 1 && N == 20) ? (const void *)mpc_group_kernel<20, 1, 16, double>
+                     : (bs == 1 && N == 10) ? (const void *)mpc_group_kernel<10, 1, 16, double>
+                     : (bs == 1 && N == 6)  ? (const void *)mpc_group_kernel<6, 1, 16, double>
+                                            : (const void *)mpc_group_kernel<6, 2, 16, double>;
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    if (bs == 1 && N == 30) hipLaunchKernelGGL((mpc_group_kernel<30, 1, 32>), g, blk, lds, stream, a);
-    else if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_group_kernel<20, 1, 16>), g, blk, lds, stream, a);
-    else if (bs == 1 && N == 10) hipLaunchKernelGGL((mpc_group_kernel<10, 1, 16>), g, blk, lds, stream, a);
-    else if (bs == 1 && N == 6) hipLaunchKernelGGL((mpc_group_kernel<6, 1, 16>), g, blk, lds, stream, a);
-    else hipLaunchKernelGGL((mpc_group_kernel<6, 2, 16>), g, blk, lds, stream, a);
+    if (bs == 1 && N == 30) hipLaunchKernelGGL((mpc_group_kernel<30, 1, 32, double>), g, blk, lds, stream, a);
+    else if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_group_kernel<20, 1, 16, double>), g, blk, lds, stream, a);
+    else if (bs == 1 && N == 10) hipLaunchKernelGGL((mpc_group_kernel<10, 1, 16, double>), g, blk, lds, stream, a);
+    else if (bs == 1 && N == 6) hipLaunchKernelGGL((mpc_group_kernel<6, 1, 16, double>), g, blk, lds, stream, a);
+    else hipLaunchKernelGGL((mpc_group_kernel<6, 2, 16, double>), g, blk, lds, stream, a);
     if (a.prof_waves) {           // the slowest waves' phase breakdown (diagnostics)
         const int64_t n = waves_needed;
         unsigned long long *h = (unsigned long long *)malloc((size_t)n * 16 * sizeof(unsigned long long));
