@@ -3,8 +3,14 @@
 Robot i of a global batch of B robots follows the Figure-8 (A=2, a=0.5, dt=0.02) with time
 offset t0_i = (i / B) * 2*pi/a (one full period over the batch) and starts at
 x_ref(t0_i) + N(0, diag(.05^2, .05^2, .1^2)).  Noise is drawn per robot from a counter-based
-generator keyed on (seed, i), so any contiguous shard of the batch is reproduced exactly
-by the rank that owns it -- no data-path collective is needed to split the batch.
+generator keyed on (seed, i), so any subset of the batch is reproduced exactly by the rank
+that owns it -- no data-path collective is needed to split the batch.
+
+Robots are dealt to ranks round-robin (rank r owns i = r, r + W, r + 2W, ...), so every
+rank's robots span the whole Figure-8 and every GPU gets the single-GPU difficulty mix.  A
+contiguous split would hand the obstacle-adjacent arcs to a few ranks: at 8 GPUs, two ranks
+would hold 17145 and 10754 robots beyond the lane-per-robot stage's cap against 0-46 on the
+others (3552 at 1 GPU), and the slowest rank sets the job's time.
 """
 import numpy as np
 
@@ -24,14 +30,24 @@ CONFIGS = {
 
 
 def shard(B_total, world, rank):
-    """Contiguous split: rank r owns [r*B/W, (r+1)*B/W)."""
+    """Contiguous split [r*B/W, (r+1)*B/W) -- kept for tools; the bench uses shard_indices."""
     lo = (B_total * rank) // world
     hi = (B_total * (rank + 1)) // world
     return lo, hi
 
 
+def shard_indices(B_total, world, rank):
+    """Round-robin split: the global robot indices rank r owns (r, r + W, ...)."""
+    return np.arange(rank, B_total, world, dtype=np.int64)
+
+
 def t0_offsets(lo, hi, B_total):
     return (np.arange(lo, hi, dtype=np.float64) / B_total) * PERIOD
+
+
+def t0_at(idx, B_total):
+    """Time offsets of the robots with global indices idx."""
+    return (np.asarray(idx, dtype=np.float64) / B_total) * PERIOD
 
 
 def _noise_aligned(lo, hi, seed, sigma=(0.05, 0.05, 0.1)):
@@ -50,6 +66,16 @@ def noise_for(lo, hi, seed, sigma=(0.05, 0.05, 0.1)):
     b0 = (lo // 65536) * 65536
     full = _noise_aligned(b0, hi, seed, sigma)
     return full[lo - b0:]
+
+
+def noise_at(idx, seed, sigma=(0.05, 0.05, 0.1)):
+    """Noise of the robots with global indices idx (same values as noise_for)."""
+    idx = np.asarray(idx, dtype=np.int64)
+    if idx.size == 0:
+        return np.empty((0, 3))
+    lo, hi = int(idx.min()) // 65536 * 65536, int(idx.max()) + 1
+    full = _noise_aligned(lo, hi, seed, sigma)
+    return full[idx - lo]
 
 
 def aggregate(dist, elapsed, counts, device="cpu"):

@@ -20,6 +20,31 @@ def test_shard_covers_batch_exactly():
         assert np.all(cov == 1)
 
 
+def test_round_robin_shards_cover_batch_and_match_global_inputs():
+    """bench.py's split: rank r owns robots r, r + W, ...; its locally generated offsets and
+    noise equal the single-process workload at those indices (no scatter needed)."""
+    for B, world in [(65536 * 8, 8), (3 * 65536 + 1000, 4), (10, 3)]:
+        cov = np.zeros(B, np.int32)
+        full_t0 = W.t0_offsets(0, B, B)
+        full_nz = W.noise_for(0, B, 7)
+        for r in range(world):
+            idx = W.shard_indices(B, world, r)
+            cov[idx] += 1
+            np.testing.assert_array_equal(W.t0_at(idx, B), full_t0[idx])
+            np.testing.assert_array_equal(W.noise_at(idx, 7), full_nz[idx])
+        assert np.all(cov == 1)
+
+
+def test_round_robin_ranks_span_the_whole_figure8():
+    """Every rank's robots cover the full period (same difficulty mix as one GPU): each
+    rank has robots in every 1/64 of the period."""
+    B, world = 65536 * 8, 8
+    for r in range(world):
+        t0 = W.t0_at(W.shard_indices(B, world, r), B)
+        hist = np.histogram(t0, bins=64, range=(0, W.PERIOD))[0]
+        assert hist.min() > 0.9 * hist.mean()
+
+
 def test_rank_inputs_equal_global_slices():
     """Rank-local generation == slice of the single-process workload (no scatter needed)."""
     B, world = 3 * 65536 + 1000, 4
@@ -42,8 +67,9 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     B_total = 65536 * world
-    lo, hi = W.shard(B_total, world, rank)
-    counts = [hi - lo - rank, rank, 0]                 # fake per-rank status counts
+    idx = W.shard_indices(B_total, world, rank)
+    lo, hi = int(idx[0]), int(idx[-1]) + 1
+    counts = [idx.size - rank, rank, 0]                # fake per-rank status counts
     elapsed, tot = W.aggregate(dist, 0.5 + rank, counts, device="cpu")
     q.put((rank, lo, hi, elapsed, tot))
     dist.barrier()
@@ -64,7 +90,7 @@ def test_gloo_two_ranks_aggregate():
         p.join(30)
         assert p.exitcode == 0
     B_total = 65536 * world
-    assert res[0][1] == 0 and res[-1][2] == B_total and res[0][2] == res[1][1]
+    assert [r[1] for r in res] == [0, 1] and res[-1][2] == B_total     # round-robin: r, r+W, ...
     for r in res:
         assert r[3] == 0.5 + (world - 1)                # slowest rank's time on every rank
         assert r[4] == [B_total - 1, 1, 0]              # status counts summed over ranks
