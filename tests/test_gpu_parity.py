@@ -222,6 +222,26 @@ def test_mpc_full_config3_vs_cpu_port(rm):
     assert np.array_equal(out["slack_used"][ok], ref["slack_used"][ok])
 
 
+def test_mpc_lti_full_batch_vs_cpu_port(rm):
+    """MPCController.solve (absolute-state LTI, mpc_node's path) on config 3's 65536 robots:
+    every robot against the C restatement (generic kernel; fallback robots compared by
+    status)."""
+    B, N = 65536, 20
+    t0 = (np.arange(B) / B) * (2 * np.pi / 0.5)
+    x0, xr, ur = _workload(N, B, 1, t0=t0)
+    obs = ompc.default_obstacles()
+    p = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02,
+                              ltv=False)
+    out = rm.batch.mpc_solve_batch(p, x0, xr, ur, obs)
+    cp = cpu.mpc_params(N, (15, 15, 50), (.1, .1), (30, 30, 40), 0.3, 5000., 2., 3., 0.02, ltv=False)
+    ref = cpu.mpc_solve_batch(cp, x0, xr, ur, obs, threads=8)
+    ok = (out["status"] == 0) & (ref["status"] == 0)
+    assert ok.mean() >= 0.999
+    d = np.abs(out["u_seq"] - ref["u_seq"]).max(axis=(1, 2))
+    assert np.all(d[ok] <= 1e-9), d[ok].max()
+    np.testing.assert_allclose(out["x_pred"][ok], ref["x_pred"][ok], atol=1e-9, rtol=0)
+
+
 @pytest.mark.parametrize("tail", ["group", "dense"])
 def test_mpc_tail_only_full_batch(rm, monkeypatch, tail):
     """RMPC_FAST_CAP=0: every one of BASELINE config 3's 65536 robots goes through the tail
