@@ -279,6 +279,34 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
     const bool hard = !p->soft && n_obs > 0;
     const bool fast = p->formulation == RMPC_LTV && !hard && rmpc_mpc_fast_supported(p->horizon, bs, p->precision) &&
                       !getenv("RMPC_DISABLE_FAST");
+    // LTI (MPCController.solve, mpc_node's path), fp64: every robot through the lane-group
+    // kernel from a cold start (RMPC_LTI_GENERIC=1: the generic kernel alone), what it does
+    // not certify through the LDS generic kernel
+    const bool lti_group = p->formulation == RMPC_LTI && !f32 && !hard && !getenv("RMPC_LTI_GENERIC") &&
+                           rmpc_mpc_group_supported(p->horizon, 1, n_obs);
+    if (lti_group) {
+        HIP_TRY(c->retry.ensure((size_t)B * sizeof(int32_t)));
+        HIP_TRY(c->retry2.ensure((size_t)B * sizeof(int32_t)));
+        HIP_TRY(c->retry_count.ensure(256));
+        HIP_TRY(hipMemsetAsync(c->retry_count.p, 0, 64, s));
+        const int32_t *list = index, *list_n = count;
+        if (!index) {                                      // the whole batch: 0..B-1
+            HIP_TRY(rmpc_launch_iota(B, (int32_t *)c->retry.p, (int32_t *)c->retry_count.p, s));
+            list = (const int32_t *)c->retry.p;
+            list_n = (const int32_t *)c->retry_count.p;
+        }
+        int32_t *cnt2 = (int32_t *)c->retry_count.p + 8;
+        const int cap = getenv("RMPC_LTI_CAP") ? atoi(getenv("RMPC_LTI_CAP")) : 11;
+        HIP_TRY(rmpc_launch_mpc_group(d, p->horizon, 1, n_obs, B, x0, x_refs, ref_rows, u_refs, uref_rows,
+                                      obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
+                                      list, list_n, (int32_t *)c->retry2.p, cnt2, cap, nullptr, s, nullptr,
+                                      false, true));
+        dbg_sync(s, "group (LTI)");
+        HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
+                                    step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
+                                    c->ws.p, (const int32_t *)c->retry2.p, cnt2, s, rmpc_mpc_lds_lanes(L)));
+        return RMPC_OK;
+    }
     if (!fast && f32)                      // fp32 arithmetic: the generic kernel on a float record
         HIP_TRY(rmpc_launch_mpc_f32(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
                                     step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,

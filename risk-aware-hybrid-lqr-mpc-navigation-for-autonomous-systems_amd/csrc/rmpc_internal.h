@@ -77,7 +77,8 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
                                  double *cost, int32_t *status, uint8_t *slack_used, int32_t *iters,
                                  const int32_t *index, const int32_t *count, int32_t *retry,
                                  int32_t *retry_count, int pdas_cap, const uint32_t *warm,
-                                 hipStream_t stream, unsigned long long *prof = nullptr, bool f32 = false);
+                                 hipStream_t stream, unsigned long long *prof = nullptr, bool f32 = false,
+                                 bool lti = false);
 
 hipError_t rmpc_launch_mpc_f64(const MpcDevParams &prm, const MpcLayout &L, int64_t B,
                                const double *x0, const double *x_refs, int ref_rows,
@@ -130,6 +131,7 @@ hipError_t rmpc_launch_plant(int64_t B, const double *x, const double *u, double
 hipError_t rmpc_launch_figure8_table(int64_t B, const int32_t *start, int32_t k, int rows, int32_t table_len,
                                      double A, double a, double dt, double *x_refs, double *u_refs,
                                      hipStream_t stream);
+hipError_t rmpc_launch_iota(int64_t B, int32_t *idx, int32_t *count, hipStream_t stream);
 hipError_t rmpc_launch_ref_offsets(int64_t B, const int32_t *start, int32_t k, int32_t last, int32_t *off,
                                    hipStream_t stream);
 hipError_t rmpc_launch_rollout_init(int64_t B, const int32_t *start, const double *x0, int32_t table_len,

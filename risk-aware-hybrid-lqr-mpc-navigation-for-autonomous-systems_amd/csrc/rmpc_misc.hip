@@ -187,6 +187,14 @@ __global__ __launch_bounds__(256) void figure8_table_kernel(int64_t B, const int
     fig8_point(A, a, dt, (double)j * dt, xr + 3 * g, ur + 2 * g);
 }
 
+// identity robot list 0..B-1 and its device-side length (whole-batch launches of the
+// list-driven kernels)
+__global__ __launch_bounds__(256) void iota_kernel(int64_t B, int32_t *idx, int32_t *count) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) *count = (int32_t)B;
+    if (i < B) idx[i] = (int32_t)i;
+}
+
 // per-robot first reference row of rollout step k in the end-padded table
 __global__ __launch_bounds__(256) void ref_offsets_kernel(int64_t B, const int32_t *start, int32_t k, int32_t last,
                                                           int32_t *off) {
@@ -293,6 +301,12 @@ hipError_t rmpc_launch_figure8_table(int64_t B, const int32_t *start, int32_t k,
     if (B <= 0) return hipSuccess;
     hipLaunchKernelGGL(figure8_table_kernel, dim3(nblk(B * rows, 256)), dim3(256), 0, stream, B, start, k, rows,
                        table_len, A, a, dt, x_refs, u_refs);
+    return hipGetLastError();
+}
+
+hipError_t rmpc_launch_iota(int64_t B, int32_t *idx, int32_t *count, hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(iota_kernel, dim3(nblk(B, 256)), dim3(256), 0, stream, B, idx, count);
     return hipGetLastError();
 }
 

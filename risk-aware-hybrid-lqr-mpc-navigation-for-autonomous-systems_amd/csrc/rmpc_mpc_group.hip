@@ -83,7 +83,8 @@ struct GRec {
     static constexpr int FR = GR + 2 * NB;         // hinge forces per step [N][2]
     static constexpr int ZF = FR + 2 * N;          // certified inputs, kept for the final write [2NB]
     static constexpr int XF = ZF + 2 * NB;         // certified trajectory [N+1][3]
-    static constexpr int INT = XF + 3 * (N + 1);   // uint32: HF [N], BF [NB], NHF [N], NBF [NB]
+    static constexpr int XR = XF + 3 * (N + 1);    // LTI: reference states (absolute form) [N+1][3]
+    static constexpr int INT = XR + 3 * (N + 1);   // uint32: HF [N], BF [NB], NHF [N], NBF [NB]
     static constexpr int INTN = ((2 * N + 2 * NB) * 4 + (int)sizeof(T) - 1) / (int)sizeof(T);
     static constexpr int HR = INT + (INTN + 1) / 2 * 2;     // hinge rows [3][no][N] (runtime no)
     __host__ __device__ static int size(int no) {
@@ -122,7 +123,10 @@ enum { PH_PDAS = 0, PH_PN = 1, PH_DONE = 2, PH_IDLE = 3 };
 // Stores that only some groups may make (GSTM) select a private junk slot instead.
 __shared__ double grp_junk[64];
 
-template <int N, int BS, int G, typename T>
+// LTI: MPCController.solve (mpc_controller.py:150-314) -- absolute states tracking the
+// (padded) references, ONE linearisation at the first reference, |u| box, rows on absolute
+// positions; no unwrap, ramp or step count.  Otherwise solve_with_ltv (:345-522).
+template <int N, int BS, int G, typename T, bool LTI>
 __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
                                             int t, bool have, int gl, int grp) {
     constexpr int NB = (N + BS - 1) / BS;
@@ -171,67 +175,112 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
 #define FR(c, k) base[RC::FR + 2 * (k) + (c)]
 #define ZF(i) base[RC::ZF + (i)]
 #define XF(k, d) base[RC::XF + 3 * (k) + (d)]
+#define XR(k, d) base[RC::XR + 3 * (k) + (d)]
 #define HF(k) reinterpret_cast<uint32_t *>(base + RC::INT)[(k)]
 #define BF(j) reinterpret_cast<uint32_t *>(base + RC::INT)[N + (j)]
 #define NHF(k) reinterpret_cast<uint32_t *>(base + RC::INT)[N + NB + (k)]
 #define NBF(j) reinterpret_cast<uint32_t *>(base + RC::INT)[2 * N + NB + (j)]
 
-    // ---- setup (mpc_controller.py:391-468): unwrap (sequential, every lane), then the
-    // linearisation and the hinge rows of this lane's steps, the blocked box per block
-    double thl[KPL];
-    double corr = 0.0, prev = xr[2], th0 = 0.0;
-#pragma unroll
-    for (int k = 0; k < N; k++) {
-        const double th = xr[3 * k + 2];
-        if (k > 0) corr += unwrap_step(prev, th);
-        prev = th;
-        const double thu = th + corr;
-        if (k == 0) th0 = thu;
-        if (k % G == gl) thl[k / G] = thu;
-    }
     bool fin = true;
-#pragma unroll
-    for (int i = 0; i < KPL; i++) {
-        const int k = gl + G * i;
-        if (k < N) {
-            double sn, cs;
-            sincos(thl[i], &sn, &cs);
-            const double v = ur[2 * k], w = ur[2 * k + 1];
-            const double vr = fabs(v) > 0.01 ? v : 0.1;                    // :425
-            STG(0, k) = -vr * sn * dt;
-            STG(1, k) = vr * cs * dt;
-            STG(2, k) = cs * dt;
-            STG(3, k) = sn * dt;
-            STG(4, k) = v;
-            STG(5, k) = w;
-            const T px = (T)xr[3 * k], py = (T)xr[3 * k + 1];
-            fin = fin && isfinite(sn + cs + v + w + px + py);
-            for (int o = 0; o < no; o++) {
-                T n0, n1, hb;
-                // (in T, from the same rounded inputs as the lane-per-robot kernel's rows)
-                if (!hinge_row_fast(px, py, (T)a.obs[3 * o], (T)a.obs[3 * o + 1], (T)(p.d_safe + a.obs[3 * o + 2]),
-                                    n0, n1, hb)) {
-                    n0 = 0; n1 = 0; hb = (T)(sizeof(T) == 8 ? -1e300 : -1e30);   // row not kept
+    T d0, d1, d2;
+    if constexpr (LTI) {
+        // ---- setup (mpc_controller.py:172-270): references padded with their last row,
+        // linearisation at (u_ref[0,0] guarded, theta_ref[0]), |u| box
+        const double v = ur[0];
+        const double vr = fabs(v) > 0.01 ? v : 0.1;                        // :186
+        double sn, cs;
+        sincos(xr[2], &sn, &cs);
+        for (int k = gl; k <= N; k += G) {
+            const int kr = k < a.ref_rows ? k : a.ref_rows - 1;
+            const double px = xr[3 * kr], py = xr[3 * kr + 1], th = xr[3 * kr + 2];
+            XR(k, 0) = (T)px; XR(k, 1) = (T)py; XR(k, 2) = (T)th;
+            fin = fin && isfinite(px + py + th);
+            if (k < N) {
+                STG(0, k) = -vr * sn * dt;
+                STG(1, k) = vr * cs * dt;
+                STG(2, k) = cs * dt;
+                STG(3, k) = sn * dt;
+                STG(4, k) = (T)0;
+                STG(5, k) = (T)0;
+                for (int o = 0; o < no; o++) {                              // :238-270
+                    const double ox = a.obs[3 * o], oy = a.obs[3 * o + 1];
+                    const double ddx = px - ox, ddy = py - oy;
+                    const double dist = sqrt(ddx * ddx + ddy * ddy);
+                    if (dist > 0.01) {
+                        const double nx = ddx / dist, ny = ddy / dist;
+                        HN0(o, k) = (T)nx;
+                        HN1(o, k) = (T)ny;
+                        HB(o, k) = (T)(p.d_safe + a.obs[3 * o + 2] + nx * ox + ny * oy);
+                    } else {
+                        HN0(o, k) = 0; HN1(o, k) = 0; HB(o, k) = (T)(sizeof(T) == 8 ? -1e300 : -1e30);
+                    }
                 }
-                HN0(o, k) = n0;
-                HN1(o, k) = n1;
-                HB(o, k) = hb;
             }
         }
-    }
-    for (int j = gl; j < NB; j += G) {                                      // :431-436
-        double lo0 = -1e300, hi0 = 1e300, lo1 = -1e300, hi1 = 1e300;
-        for (int k = j * BS; k < (j + 1) * BS && k < N; k++) {
-            lo0 = fmax(lo0, -p.v_max - ur[2 * k]);
-            hi0 = fmin(hi0, p.v_max - ur[2 * k]);
-            lo1 = fmax(lo1, -p.omega_max - ur[2 * k + 1]);
-            hi1 = fmin(hi1, p.omega_max - ur[2 * k + 1]);
+        for (int j = gl; j < NB; j += G) {                                  // :230-234
+            BND(0, j) = -p.v_max; BND(1, j) = p.v_max; BND(2, j) = -p.omega_max; BND(3, j) = p.omega_max;
         }
-        BND(0, j) = lo0; BND(1, j) = hi0; BND(2, j) = lo1; BND(3, j) = hi1;
+        fin = fin && isfinite(sn + cs + vr);
+        const double *x0p = a.x0 + 3 * b;
+        d0 = (T)x0p[0]; d1 = (T)x0p[1]; d2 = (T)x0p[2];
+    } else {
+        // ---- setup (mpc_controller.py:391-468): unwrap (sequential, every lane), then the
+        // linearisation and the hinge rows of this lane's steps, the blocked box per block
+        double thl[KPL];
+        double corr = 0.0, prev = xr[2], th0 = 0.0;
+    #pragma unroll
+        for (int k = 0; k < N; k++) {
+            const double th = xr[3 * k + 2];
+            if (k > 0) corr += unwrap_step(prev, th);
+            prev = th;
+            const double thu = th + corr;
+            if (k == 0) th0 = thu;
+            if (k % G == gl) thl[k / G] = thu;
+        }
+    #pragma unroll
+        for (int i = 0; i < KPL; i++) {
+            const int k = gl + G * i;
+            if (k < N) {
+                double sn, cs;
+                sincos(thl[i], &sn, &cs);
+                const double v = ur[2 * k], w = ur[2 * k + 1];
+                const double vr = fabs(v) > 0.01 ? v : 0.1;                    // :425
+                STG(0, k) = -vr * sn * dt;
+                STG(1, k) = vr * cs * dt;
+                STG(2, k) = cs * dt;
+                STG(3, k) = sn * dt;
+                STG(4, k) = v;
+                STG(5, k) = w;
+                const T px = (T)xr[3 * k], py = (T)xr[3 * k + 1];
+                fin = fin && isfinite(sn + cs + v + w + px + py);
+                for (int o = 0; o < no; o++) {
+                    T n0, n1, hb;
+                    // (in T, from the same rounded inputs as the lane-per-robot kernel's rows)
+                    if (!hinge_row_fast(px, py, (T)a.obs[3 * o], (T)a.obs[3 * o + 1], (T)(p.d_safe + a.obs[3 * o + 2]),
+                                        n0, n1, hb)) {
+                        n0 = 0; n1 = 0; hb = (T)(sizeof(T) == 8 ? -1e300 : -1e30);   // row not kept
+                    }
+                    HN0(o, k) = n0;
+                    HN1(o, k) = n1;
+                    HB(o, k) = hb;
+                }
+            }
+        }
+        for (int j = gl; j < NB; j += G) {                                      // :431-436
+            double lo0 = -1e300, hi0 = 1e300, lo1 = -1e300, hi1 = 1e300;
+            for (int k = j * BS; k < (j + 1) * BS && k < N; k++) {
+                lo0 = fmax(lo0, -p.v_max - ur[2 * k]);
+                hi0 = fmin(hi0, p.v_max - ur[2 * k]);
+                lo1 = fmax(lo1, -p.omega_max - ur[2 * k + 1]);
+                hi1 = fmin(hi1, p.omega_max - ur[2 * k + 1]);
+            }
+            BND(0, j) = lo0; BND(1, j) = hi0; BND(2, j) = lo1; BND(3, j) = hi1;
+        }
+        const double *x0p = a.x0 + 3 * b;
+        const double x0a = th0 + wrap_pi(x0p[2] - th0);                        // :397-401
+        d0 = (T)(x0p[0] - xr[0]); d1 = (T)(x0p[1] - xr[1]); d2 = (T)(x0a - th0);
+
     }
-    const double *x0p = a.x0 + 3 * b;
-    const double x0a = th0 + wrap_pi(x0p[2] - th0);                        // :397-401
-    const T d0 = (T)(x0p[0] - xr[0]), d1 = (T)(x0p[1] - xr[1]), d2 = (T)(x0a - th0);
     fin = fin && isfinite(d0 + d1 + d2);
     int it0 = 0;                      // iterations of the previous stage (reported in iters)
     {
@@ -261,10 +310,12 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         int u = 0;
         for (int k = gl; k <= N; k += G) {
             const T y0 = XS(k, 0), y1 = XS(k, 1), y2 = XS(k, 2);
+            // tracking error: the state deviation (LTV) or state minus reference (LTI)
+            const T e0 = LTI ? y0 - XR(k, 0) : y0, e1 = LTI ? y1 - XR(k, 1) : y1, e2 = LTI ? y2 - XR(k, 2) : y2;
             if (k == N) {
-                jl += P0 * y0 * y0 + P1 * y1 * y1 + P2 * y2 * y2;
+                jl += P0 * e0 * e0 + P1 * e1 * e1 + P2 * e2 * e2;
             } else {
-                jl += Q0 * y0 * y0 + Q1 * y1 * y1 + Q2 * y2 * y2;
+                jl += Q0 * e0 * e0 + Q1 * e1 * e1 + Q2 * e2 * e2;
                 const int j = k / BS;
                 const T uu0 = base[zoff + 2 * j] + STG(4, k), uu1 = base[zoff + 2 * j + 1] + STG(5, k);
                 jl += R0 * uu0 * uu0 + R1 * uu1 * uu1;
@@ -316,7 +367,8 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         refresh();
         // per-step stage weights from the active rows (lane-parallel over steps)
         for (int k = gl; k < N; k += G) {
-            T q00 = Q0, q01 = 0.0, q11 = Q1, qv0 = -Q0 * (T)0, qv1 = -Q1 * (T)0;
+            T q00 = Q0, q01 = 0.0, q11 = Q1;
+            T qv0 = -Q0 * (LTI ? XR(k, 0) : (T)0), qv1 = -Q1 * (LTI ? XR(k, 1) : (T)0);
             const uint32_t h = HF(k);
             if (k > 0 && h) {
                 for (int o = 0; o < no; o++) {
@@ -330,6 +382,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
                 }
             }
             WQ(k, 0) = q00; WQ(k, 1) = q01; WQ(k, 2) = q11; WQ(k, 3) = qv0; WQ(k, 4) = qv1;
+            if constexpr (LTI) WQ(k, 5) = -Q2 * XR(k, 2);
         }
         __syncthreads();
         GPROF(2);
@@ -337,7 +390,11 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         // backward block Riccati sweep (uniform within the group)
         RicV<T> V;
         V.P00 = P0; V.P01 = 0; V.P02 = 0; V.P11 = P1; V.P12 = 0; V.P22 = P2;
-        V.p0 = -P0 * 0.0; V.p1 = -P1 * 0.0; V.p2 = -P2 * 0.0;
+        if constexpr (LTI) {
+            V.p0 = -P0 * XR(N, 0); V.p1 = -P1 * XR(N, 1); V.p2 = -P2 * XR(N, 2);
+        } else {
+            V.p0 = -P0 * 0.0; V.p1 = -P1 * 0.0; V.p2 = -P2 * 0.0;
+        }
         if constexpr (BS == 1) {
             // single-step blocks, software-pipelined: step j-1's record is loaded while step j
             // computes (the scheduler does not hoist LDS loads across unrolled steps itself)
@@ -361,7 +418,8 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
                 __builtin_amdgcn_sched_barrier(0);
                 const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
                 T Gv[8];
-                V = ric_step1_bf(V, c[0], c[1], c[2], c[3], dt, c[6], c[7], c[8], Q2, c[9], c[10], -Q2 * (T)0, R0, R1,
+                V = ric_step1_bf(V, c[0], c[1], c[2], c[3], dt, c[6], c[7], c[8], Q2, c[9], c[10],
+                                 LTI ? c[11] : -Q2 * (T)0, R0, R1,
                                  R0 * c[4], R1 * c[5], bf0, bf1, bf0 == 1 ? c[12] : c[13], bf1 == 1 ? c[14] : c[15], Gv);
 #pragma unroll
                 for (int q = 0; q < 8; q++) GST(GN(j, q), Gv[q]);
@@ -377,7 +435,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
 #pragma unroll
                 for (int k = k1 - 1; k >= k0; k--) {
                     ric_step(W, STG(0, k), STG(1, k), STG(2, k), STG(3, k), dt, WQ(k, 0), WQ(k, 1), WQ(k, 2), Q2,
-                             WQ(k, 3), WQ(k, 4), -Q2 * (T)0, R0, R1, R0 * STG(4, k), R1 * STG(5, k));
+                             WQ(k, 3), WQ(k, 4), LTI ? WQ(k, 5) : -Q2 * (T)0, R0, R1, R0 * STG(4, k), R1 * STG(5, k));
                 }
                 V = ric_block_bf(W, bf0, bf1, bf0 == 1 ? BND(0, j) : BND(1, j), bf1 == 1 ? BND(2, j) : BND(3, j), Gv);
 #pragma unroll
@@ -479,7 +537,9 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         }
         __syncthreads();
         refresh();
-        T l0 = 2 * P0 * XS(N, 0), l1 = 2 * P1 * XS(N, 1), l2 = 2 * P2 * XS(N, 2);
+        T l0 = 2 * P0 * (LTI ? XS(N, 0) - XR(N, 0) : XS(N, 0));
+        T l1 = 2 * P1 * (LTI ? XS(N, 1) - XR(N, 1) : XS(N, 1));
+        T l2 = 2 * P2 * (LTI ? XS(N, 2) - XR(N, 2) : XS(N, 2));
 #pragma unroll
         for (int j = NB - 1; j >= 0; j--) {
             T g0 = 0.0, g1 = 0.0;
@@ -488,9 +548,9 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
             for (int k = ((j + 1) * BS < N ? (j + 1) * BS : N) - 1; k >= j * BS; k--) {
                 g0 += STG(2, k) * l0 + STG(3, k) * l1 + 2 * R0 * (z0 + STG(4, k));
                 g1 += dt * l2 + 2 * R1 * (z1 + STG(5, k));
-                const T m0 = 2 * Q0 * XS(k, 0) + l0 + (k > 0 ? FR(0, k) : (T)0);
-                const T m1 = 2 * Q1 * XS(k, 1) + l1 + (k > 0 ? FR(1, k) : (T)0);
-                const T m2 = 2 * Q2 * XS(k, 2) + STG(0, k) * l0 + STG(1, k) * l1 + l2;
+                const T m0 = 2 * Q0 * (LTI ? XS(k, 0) - XR(k, 0) : XS(k, 0)) + l0 + (k > 0 ? FR(0, k) : (T)0);
+                const T m1 = 2 * Q1 * (LTI ? XS(k, 1) - XR(k, 1) : XS(k, 1)) + l1 + (k > 0 ? FR(1, k) : (T)0);
+                const T m2 = 2 * Q2 * (LTI ? XS(k, 2) - XR(k, 2) : XS(k, 2)) + STG(0, k) * l0 + STG(1, k) * l1 + l2;
                 l0 = m0; l1 = m1; l2 = m2;
             }
             GSTM(GR(2 * j), g0, m); GSTM(GR(2 * j + 1), g1, m);
@@ -649,7 +709,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
     if (__any(done_ok)) {
         refresh();
         if (done_ok) {
-            const int sc = a.step_count ? a.step_count[b] : 0;
+            const int sc = (!LTI && a.step_count) ? a.step_count[b] : 0;
             for (int k = gl; k < N; k += G) {
                 const int j = k / BS;
                 // fp64: u = du + u_ref in the record; fp32: du + the fp64 u_ref (only the
@@ -657,7 +717,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
                 constexpr bool F64 = sizeof(T) == 8;
                 const double v0 = F64 ? (double)(ZF(2 * j) + STG(4, k)) : (double)ZF(2 * j) + ur[2 * k];
                 double v1 = F64 ? (double)(ZF(2 * j + 1) + STG(5, k)) : (double)ZF(2 * j + 1) + ur[2 * k + 1];
-                if (k == 0 && sc < p.ramp_up_steps) {                      // :502-505
+                if (!LTI && k == 0 && sc < p.ramp_up_steps) {              // :502-505 (LTV only)
                     const double lim = p.omega_max * ((double)(sc + 1) / (double)p.ramp_up_steps);
                     v1 = clampv(v1, -lim, lim);
                 }
@@ -673,13 +733,17 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
             if (a.x_pred) {                                                 // :497
                 for (int k = gl; k <= N; k += G) {
                     double *xp = a.x_pred + ((size_t)b * (N + 1) + k) * 3;
-                    xp[0] = (double)XF(k, 0) + xr[3 * k];
-                    xp[1] = (double)XF(k, 1) + xr[3 * k + 1];
-                    xp[2] = (double)XF(k, 2) + xr[3 * k + 2];
+                    if constexpr (LTI) {                                    // absolute states
+                        xp[0] = (double)XF(k, 0); xp[1] = (double)XF(k, 1); xp[2] = (double)XF(k, 2);
+                    } else {
+                        xp[0] = (double)XF(k, 0) + xr[3 * k];
+                        xp[1] = (double)XF(k, 1) + xr[3 * k + 1];
+                        xp[2] = (double)XF(k, 2) + xr[3 * k + 2];
+                    }
                 }
             }
             if (gl == 0) {
-                if (a.step_count) a.step_count[b] = sc + 1;                 // :507
+                if (!LTI && a.step_count) a.step_count[b] = sc + 1;         // :507 (LTV only)
                 if (a.cost) a.cost[b] = J_out;
                 if (a.slack_used) a.slack_used[b] = (uint8_t)used_out;
                 a.status[b] = RMPC_OPTIMAL;
@@ -711,6 +775,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
 #undef FR
 #undef ZF
 #undef XF
+#undef XR
 #undef HF
 #undef BF
 #undef NHF
@@ -724,7 +789,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
 // tail's run time).  A persistent variant that looped over rounds faulted from its second
 // round on (every robot's accesses in bounds, checked with RMPC_GROUP_CHECK), so there is
 // no round loop.
-template <int N, int BS, int G, typename T>
+template <int N, int BS, int G, typename T, bool LTI>
 __global__ __launch_bounds__(64, 1) void mpc_group_kernel(GroupArgs a) {
     constexpr int NB = (N + BS - 1) / BS, RPW = 64 / G;
     extern __shared__ double lds_raw[];
@@ -736,7 +801,7 @@ __global__ __launch_bounds__(64, 1) void mpc_group_kernel(GroupArgs a) {
     const int t0 = blockIdx.x * RPW;
     if (t0 >= cnt) return;
     const int t = t0 + grp;
-    group_solve<N, BS, G, T>(a, lds + grp * rec, t, t < cnt, gl, grp);
+    group_solve<N, BS, G, T, LTI>(a, lds + grp * rec, t, t < cnt, gl, grp);
 }
 
 // lanes per robot: 16 (four robots per wave) while the record leaves room for four waves
@@ -776,9 +841,9 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
                                  double *cost, int32_t *status, uint8_t *slack_used, int32_t *iters,
                                  const int32_t *index, const int32_t *count, int32_t *retry,
                                  int32_t *retry_count, int pdas_cap, const uint32_t *warm,
-                                 hipStream_t stream, unsigned long long *prof, bool f32) {
+                                 hipStream_t stream, unsigned long long *prof, bool f32, bool lti) {
     if (capacity <= 0) return hipSuccess;
-    if (!rmpc_mpc_group_supported(N, bs, no, f32)) return hipErrorInvalidValue;
+    if (!rmpc_mpc_group_supported(N, bs, no, f32) || (lti && bs != 1)) return hipErrorInvalidValue;
     GroupArgs a;
     a.prm = prm;
     a.no = no;
@@ -822,20 +887,22 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
     const size_t lds = (size_t)rpw * group_rec_bytes(N, bs, no, f32);
     const int64_t need = (capacity + rpw - 1) / rpw;
     const dim3 g((unsigned)need), blk(64);
-    const void *fn = (bs == 1 && N == 30)   ? (const void *)mpc_group_kernel<30, 1, 32, double>
-                     : (bs == 1 && N == 20) ? (const void *)mpc_group_kernel<20, 1, 16, double>
-                     : (bs == 1 && N == 10) ? (const void *)mpc_group_kernel<10, 1, 16, double>
-                     : (bs == 1 && N == 6)  ? (const void *)mpc_group_kernel<6, 1, 16, double>
-                                            : (const void *)mpc_group_kernel<6, 2, 16, double>;
+#define GK(n, b, g, l) (const void *)mpc_group_kernel<n, b, g, double, l>
+    const void *fn = (bs == 1 && N == 30)   ? (lti ? GK(30, 1, 32, true) : GK(30, 1, 32, false))
+                     : (bs == 1 && N == 20) ? (lti ? GK(20, 1, 16, true) : GK(20, 1, 16, false))
+                     : (bs == 1 && N == 10) ? (lti ? GK(10, 1, 16, true) : GK(10, 1, 16, false))
+                     : (bs == 1 && N == 6)  ? (lti ? GK(6, 1, 16, true) : GK(6, 1, 16, false))
+                                            : GK(6, 2, 16, false);
+#undef GK
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    if (bs == 1 && N == 30) hipLaunchKernelGGL((mpc_group_kernel<30, 1, 32, double>), g, blk, lds, stream, a);
-    else if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_group_kernel<20, 1, 16, double>), g, blk, lds, stream, a);
-    else if (bs == 1 && N == 10) hipLaunchKernelGGL((mpc_group_kernel<10, 1, 16, double>), g, blk, lds, stream, a);
-    else if (bs == 1 && N == 6) hipLaunchKernelGGL((mpc_group_kernel<6, 1, 16, double>), g, blk, lds, stream, a);
-    else hipLaunchKernelGGL((mpc_group_kernel<6, 2, 16, double>), g, blk, lds, stream, a);
+    void *args[] = {&a};
+    {
+        const hipError_t e = hipLaunchKernel(fn, g, blk, args, lds, stream);
+        if (e != hipSuccess) return e;
+    }
     if (a.prof_waves) {           // the slowest waves' phase breakdown (diagnostics)
         const int64_t n = waves_needed;
         unsigned long long *h = (unsigned long long *)malloc((size_t)n * 16 * sizeof(unsigned long long));
