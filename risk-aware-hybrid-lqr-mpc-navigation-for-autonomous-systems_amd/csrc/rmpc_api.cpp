@@ -279,11 +279,13 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
     const bool hard = !p->soft && n_obs > 0;
     const bool fast = p->formulation == RMPC_LTV && !hard && rmpc_mpc_fast_supported(p->horizon, bs, p->precision) &&
                       !getenv("RMPC_DISABLE_FAST");
-    // LTI (MPCController.solve, mpc_node's path), fp64: every robot through the lane-group
-    // kernel from a cold start (RMPC_LTI_GENERIC=1: the generic kernel alone), what it does
-    // not certify through the LDS generic kernel
-    const bool lti_group = p->formulation == RMPC_LTI && !f32 && !hard && !getenv("RMPC_LTI_GENERIC") &&
-                           rmpc_mpc_group_supported(p->horizon, 1, n_obs);
+    // fp64 without a lane-per-robot instance -- LTI (MPCController.solve, mpc_node's path),
+    // or an LTV (N, block size) the fast kernel is not built for (N = 30) -- every robot
+    // through the lane-group kernel from a cold start (RMPC_LTI_GENERIC=1: the generic kernel
+    // alone), what it does not certify through the LDS generic kernel
+    const bool lti = p->formulation == RMPC_LTI;
+    const bool lti_group = !fast && !f32 && !hard && !getenv("RMPC_LTI_GENERIC") &&
+                           rmpc_mpc_group_supported(p->horizon, lti ? 1 : bs, n_obs);
     if (lti_group) {
         HIP_TRY(c->retry.ensure((size_t)B * sizeof(int32_t)));
         HIP_TRY(c->retry2.ensure((size_t)B * sizeof(int32_t)));
@@ -297,11 +299,11 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         }
         int32_t *cnt2 = (int32_t *)c->retry_count.p + 8;
         const int cap = getenv("RMPC_LTI_CAP") ? atoi(getenv("RMPC_LTI_CAP")) : 11;
-        HIP_TRY(rmpc_launch_mpc_group(d, p->horizon, 1, n_obs, B, x0, x_refs, ref_rows, u_refs, uref_rows,
-                                      obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
-                                      list, list_n, (int32_t *)c->retry2.p, cnt2, cap, nullptr, s, nullptr,
-                                      false, true));
-        dbg_sync(s, "group (LTI)");
+        HIP_TRY(rmpc_launch_mpc_group(d, p->horizon, lti ? 1 : bs, n_obs, B, x0, x_refs, ref_rows, u_refs,
+                                      uref_rows, obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
+                                      iters, list, list_n, (int32_t *)c->retry2.p, cnt2, cap, nullptr, s, nullptr,
+                                      false, lti));
+        dbg_sync(s, "group (cold)");
         HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
                                     step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
                                     c->ws.p, (const int32_t *)c->retry2.p, cnt2, s, rmpc_mpc_lds_lanes(L)));

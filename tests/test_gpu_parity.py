@@ -154,6 +154,15 @@ def test_mpc_kernel_matches_exact_qp_oracle(rm, N, bs, scen, ltv, noise, seed, B
         assert np.all(sc == 5)
 
 
+@pytest.mark.parametrize("N,bs,scen,ltv,noise,seed,B", [CASES[1], CASES[2], CASES[4], CASES[5]])
+def test_mpc_generic_kernel_matches_exact_qp_oracle(rm, monkeypatch, N, bs, scen, ltv, noise, seed, B):
+    """The generic lane-per-robot kernel alone (RMPC_DISABLE_FAST + RMPC_LTI_GENERIC): the
+    path of (N, block size) shapes without lane-group instances and of hard constraints."""
+    monkeypatch.setenv("RMPC_DISABLE_FAST", "1")
+    monkeypatch.setenv("RMPC_LTI_GENERIC", "1")
+    test_mpc_kernel_matches_exact_qp_oracle(rm, N, bs, scen, ltv, noise, seed, B)
+
+
 HARD_CASES = [  # (N, bs, scenario, ltv, noise, seed, B): use_soft_constraints=False
     (20, 1, "default", True, (0.05, 0.05, 0.1), 7, 40),
     (20, 1, "default", True, (0.3, 0.3, 0.5), 7, 40),
