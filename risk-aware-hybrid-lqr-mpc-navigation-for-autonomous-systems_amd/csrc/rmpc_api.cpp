@@ -273,17 +273,17 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
     const MpcLayout L = rmpc_mpc_layout(p->horizon, bs, n_obs);
     HIP_TRY(ensure_ws(c, L, B));
     MpcDevParams d = to_dev(p);
+    const bool lti = p->formulation == RMPC_LTI;
     d.ref_off = ref_off;
     const bool f32 = p->precision == RMPC_F32;
     // hard half-spaces (soft = 0 with obstacles): augmented-Lagrangian rounds in the generic kernel
     const bool hard = !p->soft && n_obs > 0;
-    const bool fast = p->formulation == RMPC_LTV && !hard && rmpc_mpc_fast_supported(p->horizon, bs, p->precision) &&
+    const bool fast = !hard && rmpc_mpc_fast_supported(p->horizon, bs, p->precision, p->formulation == RMPC_LTI) &&
                       !getenv("RMPC_DISABLE_FAST");
     // fp64 without a lane-per-robot instance -- LTI (MPCController.solve, mpc_node's path),
     // or an LTV (N, block size) the fast kernel is not built for (N = 30) -- every robot
     // through the lane-group kernel from a cold start (RMPC_LTI_GENERIC=1: the generic kernel
     // alone), what it does not certify through the LDS generic kernel
-    const bool lti = p->formulation == RMPC_LTI;
     const bool lti_group = !fast && !f32 && !hard && !getenv("RMPC_LTI_GENERIC") &&
                            rmpc_mpc_group_supported(p->horizon, lti ? 1 : bs, n_obs);
     if (lti_group) {
@@ -358,7 +358,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         }
         a.prof = pc;
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[0], s));
-        HIP_TRY(rmpc_launch_mpc_fast(a, p->horizon, bs, p->precision, s));
+        HIP_TRY(rmpc_launch_mpc_fast(a, p->horizon, bs, p->precision, s, lti));
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[1], s));
         dbg_sync(s, "fast");
         const int32_t *left = (const int32_t *)c->retry.p;
@@ -366,7 +366,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         // tail: the lane-group Riccati kernel (default) or the condensed wave-per-robot one
         // (RMPC_TAIL=dense); RMPC_DISABLE_DENSE skips the tail stage altogether
         const char *tail = getenv("RMPC_TAIL");
-        const bool use_dense = tail && !strcmp(tail, "dense");
+        const bool use_dense = tail && !strcmp(tail, "dense") && !lti;   // the dense tail is LTV-only
         // tail PDAS cap before projected Newton (sweeps: 4 at N <= 20, 6 beyond -- config 4)
         const int tail_cap = getenv("RMPC_DENSE_CAP") ? atoi(getenv("RMPC_DENSE_CAP")) : (p->horizon <= 20 ? 4 : 6);
         // fp32 requests get the fp32 lane-group tail (RMPC_TAIL64=1: the fp64 one)
@@ -377,7 +377,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             HIP_TRY(rmpc_launch_mpc_group(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs, uref_rows,
                                           obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
                                           iters, left, left_n, (int32_t *)c->retry2.p, cnt2, tail_cap,
-                                          a.retry_sets, s, pc, tail32));
+                                          a.retry_sets, s, pc, tail32, lti));
             if (prof) {
                 unsigned long long h[64];
                 int32_t cn[16];
@@ -401,7 +401,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             dbg_sync(s, "group");
             left = (const int32_t *)c->retry2.p;
             left_n = cnt2;
-        } else if (rmpc_mpc_dense_supported(p->horizon, bs, n_obs) && !getenv("RMPC_DISABLE_DENSE")) {
+        } else if (!lti && rmpc_mpc_dense_supported(p->horizon, bs, n_obs) && !getenv("RMPC_DISABLE_DENSE")) {
             HIP_TRY(c->retry2.ensure((size_t)B * sizeof(int32_t)));
             int32_t *cnt2 = (int32_t *)c->retry_count.p + 8;
             HIP_TRY(rmpc_launch_mpc_dense_f64(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs,

@@ -57,7 +57,7 @@ struct MpcFastArgs {
                                      // (warm start of the next stage; may be null)
 };
 
-bool rmpc_mpc_fast_supported(int N, int bs, int prec);
+bool rmpc_mpc_fast_supported(int N, int bs, int prec, bool lti = false);
 bool rmpc_mpc_dense_supported(int N, int bs, int no);
 hipError_t rmpc_launch_mpc_dense_f64(const MpcDevParams &prm, int N, int bs, int no, int64_t capacity,
                                      const double *x0, const double *x_refs, int ref_rows,
@@ -68,7 +68,8 @@ hipError_t rmpc_launch_mpc_dense_f64(const MpcDevParams &prm, int N, int bs, int
                                      int32_t *retry_count, int32_t *next, int pdas_cap,
                                      const uint32_t *warm, hipStream_t stream,
                                      unsigned long long *prof = nullptr);
-hipError_t rmpc_launch_mpc_fast(const MpcFastArgs &a, int N, int bs, int prec, hipStream_t stream);
+hipError_t rmpc_launch_mpc_fast(const MpcFastArgs &a, int N, int bs, int prec, hipStream_t stream,
+                                bool lti = false);
 bool rmpc_mpc_group_supported(int N, int bs, int no, bool f32 = false);
 hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no, int64_t capacity,
                                  const double *x0, const double *x_refs, int ref_rows,

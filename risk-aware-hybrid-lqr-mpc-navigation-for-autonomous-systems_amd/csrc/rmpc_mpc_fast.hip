@@ -113,8 +113,15 @@ template <typename T> struct Big;
 template <> struct Big<double> { static constexpr double v = 1e300; };
 template <> struct Big<float> { static constexpr float v = 1e30f; };
 
-template <int N, int BS, typename T>
+// LTI = true: MPCController.solve (mpc_controller.py:150-314) in error coordinates
+// e_k = x_k - x_ref,k (references padded with their last row).  The LTI model applied to
+// absolute states then reads e_{k+1} = A e_k + B u_k + c_k with c_k = A x_ref,k - x_ref,k+1,
+// so the sweeps are the LTV ones plus the affine term: p += P c_k before each backward step
+// and + c_k in each forward step.  One linearisation (constants), |u| box, u_ref terms 0;
+// per-step registers S/Cs/V0 hold c_k and the V1 slot the reference heading.
+template <int N, int BS, typename T, bool LTI>
 __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
+    static_assert(!LTI || BS == 1, "LTI ignores move blocking");
     constexpr int NB = (N + BS - 1) / BS;
     constexpr int PF = 4;     // gain blocks prefetched ahead in the forward sweep
     constexpr bool F64 = sizeof(T) == 8;
@@ -159,29 +166,59 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
 #define PX(k) lds[(0 * N + (k)) * RMPC_WAVE + lane]
 #define PY(k) lds[(1 * N + (k)) * RMPC_WAVE + lane]
 #define V1(k) lds[(2 * N + (k)) * RMPC_WAVE + lane]
-    double corr = 0.0, prev = xr[2], th0 = 0.0;
     bool fin = true;
-#pragma unroll
-    for (int k = 0; k < N; k++) {
-        const double th = xr[3 * k + 2];
-        if (k > 0) corr += unwrap_step(prev, th);
-        prev = th;
-        const double thu = th + corr;
-        if (k == 0) th0 = thu;
-        double sn, cs;
-        sincos(thu, &sn, &cs);
-        S[k] = (T)sn;
-        Cs[k] = (T)cs;
-        V0[k] = (T)ur[2 * k];
-        V1(k) = (T)ur[2 * k + 1];
-        PX(k) = (T)xr[3 * k];
-        PY(k) = (T)xr[3 * k + 1];
-        fin = fin && isfinite(S[k] + Cs[k] + V0[k] + V1(k) + PX(k) + PY(k));
-        __builtin_amdgcn_sched_barrier(0);
-    }
+    T d0, d1, d2;
+    T la0 = 0, la1 = 0, lb0 = 0, lb1 = 0;        // LTI: the one linearisation
+    double xsN0 = 0, xsN1 = 0, xsN2 = 0;          // LTI: terminal reference state
     const double *x0p = a.x0 + 3 * b;
-    const double x0a = th0 + wrap_pi(x0p[2] - th0);                // :397-401
-    const T d0 = (T)(x0p[0] - xr[0]), d1 = (T)(x0p[1] - xr[1]), d2 = (T)(x0a - th0);
+    if constexpr (LTI) {
+        const double v = ur[0];
+        const double vr = fabs(v) > 0.01 ? v : 0.1;                 // :186
+        double sn, cs;
+        sincos(xr[2], &sn, &cs);
+        const double A0 = -vr * sn * p.dt, A1 = vr * cs * p.dt;
+        la0 = (T)A0; la1 = (T)A1; lb0 = (T)(cs * p.dt); lb1 = (T)(sn * p.dt);
+        const int last = a.ref_rows - 1;
+#pragma unroll
+        for (int k = 0; k < N; k++) {                              // :172-183 padding
+            const int kr = k < last ? k : last, kn = k + 1 < last ? k + 1 : last;
+            const double px = xr[3 * kr], py = xr[3 * kr + 1], th = xr[3 * kr + 2];
+            S[k] = (T)(px + A0 * th - xr[3 * kn]);
+            Cs[k] = (T)(py + A1 * th - xr[3 * kn + 1]);
+            V0[k] = (T)(th - xr[3 * kn + 2]);
+            V1(k) = (T)th;
+            PX(k) = (T)px;
+            PY(k) = (T)py;
+            fin = fin && isfinite(S[k] + Cs[k] + V0[k] + V1(k));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const int kN = N < last ? N : last;
+        xsN0 = xr[3 * kN]; xsN1 = xr[3 * kN + 1]; xsN2 = xr[3 * kN + 2];
+        d0 = (T)(x0p[0] - xr[0]); d1 = (T)(x0p[1] - xr[1]); d2 = (T)(x0p[2] - xr[2]);
+        fin = fin && isfinite(sn + cs + vr + xsN0 + xsN1 + xsN2);
+    } else {
+        double corr = 0.0, prev = xr[2], th0 = 0.0;
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            const double th = xr[3 * k + 2];
+            if (k > 0) corr += unwrap_step(prev, th);
+            prev = th;
+            const double thu = th + corr;
+            if (k == 0) th0 = thu;
+            double sn, cs;
+            sincos(thu, &sn, &cs);
+            S[k] = (T)sn;
+            Cs[k] = (T)cs;
+            V0[k] = (T)ur[2 * k];
+            V1(k) = (T)ur[2 * k + 1];
+            PX(k) = (T)xr[3 * k];
+            PY(k) = (T)xr[3 * k + 1];
+            fin = fin && isfinite(S[k] + Cs[k] + V0[k] + V1(k) + PX(k) + PY(k));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const double x0a = th0 + wrap_pi(x0p[2] - th0);            // :397-401
+        d0 = (T)(x0p[0] - xr[0]); d1 = (T)(x0p[1] - xr[1]); d2 = (T)(x0a - th0);
+    }
     fin = fin && isfinite(d0 + d1 + d2);
 
     HingeFlags<N> Hf;                 // hinge-row active flags of step k (bit o)
@@ -241,15 +278,29 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                         cx = nx; cy = ny; cs = ns;
                     }
                 }
-                const T vr = fabs(V0[k]) > (T)0.01 ? V0[k] : (T)0.1;     // :425
-                const T a0 = -vr * S[k] * dt, a1 = vr * Cs[k] * dt;
-                const T b0 = Cs[k] * dt, b1 = S[k] * dt;
-                const T lo0 = -vmax - V0[k], hi0 = vmax - V0[k];       // :431-436
-                const T lo1 = -omax - V1(k), hi1 = omax - V1(k);
+                T a0, a1, b0, b1, lo0, hi0, lo1, hi1, us0, us1;
+                if constexpr (LTI) {
+                    a0 = la0; a1 = la1; b0 = lb0; b1 = lb1;
+                    lo0 = -vmax; hi0 = vmax; lo1 = -omax; hi1 = omax;           // :230-234
+                    us0 = 0; us1 = 0;
+                    // affine term of the error dynamics: V(Ae + Bu + c) = V'(Ae + Bu), p' = p + P c
+                    const T c0 = S[k], c1 = Cs[k], c2 = V0[k];
+                    const T p0n = V.p0 + V.P00 * c0 + V.P01 * c1 + V.P02 * c2;
+                    const T p1n = V.p1 + V.P01 * c0 + V.P11 * c1 + V.P12 * c2;
+                    const T p2n = V.p2 + V.P02 * c0 + V.P12 * c1 + V.P22 * c2;
+                    V.p0 = p0n; V.p1 = p1n; V.p2 = p2n;
+                } else {
+                    const T vr = fabs(V0[k]) > (T)0.01 ? V0[k] : (T)0.1;     // :425
+                    a0 = -vr * S[k] * dt; a1 = vr * Cs[k] * dt;
+                    b0 = Cs[k] * dt; b1 = S[k] * dt;
+                    lo0 = -vmax - V0[k]; hi0 = vmax - V0[k];                 // :431-436
+                    lo1 = -omax - V1(k); hi1 = omax - V1(k);
+                    us0 = V0[k]; us1 = V1(k);
+                }
                 const uint32_t bfj = Bf.get(j);
                 const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
                 V = ric_step1_bf(V, a0, a1, b0, b1, dt, q00, q01, q11, Q2, qv0, qv1, qv2, R0, R1,
-                                 R0 * V0[k], R1 * V1(k), bf0, bf1, bf0 == 1 ? lo0 : hi0, bf1 == 1 ? lo1 : hi1, G);
+                                 R0 * us0, R1 * us1, bf0, bf1, bf0 == 1 ? lo0 : hi0, bf1 == 1 ? lo1 : hi1, G);
             } else {
                 RicW<T> W = ric_open(V);
                 T lo0 = -BIG, hi0 = BIG, lo1 = -BIG, hi1 = BIG;
@@ -317,7 +368,9 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             const int k0 = j * BS;
             const int k1 = (k0 + BS < N) ? k0 + BS : N;
             T lo0 = -BIG, hi0 = BIG, lo1 = -BIG, hi1 = BIG;
-            if constexpr (BS == 1) {
+            if constexpr (LTI) {
+                lo0 = -vmax; hi0 = vmax; lo1 = -omax; hi1 = omax;
+            } else if constexpr (BS == 1) {
                 lo0 = -vmax - V0[k0]; hi0 = vmax - V0[k0];
                 lo1 = -omax - V1(k0); hi1 = omax - V1(k0);
             } else {
@@ -341,7 +394,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
 #pragma unroll
             for (int k = k0; k < k1; k++) {
                 J += Q0 * x0 * x0 + Q1 * x1 * x1 + Q2 * x2 * x2;
-                const T uu0 = u0v + V0[k], uu1 = u1v + V1(k);
+                const T uu0 = LTI ? u0v : u0v + V0[k], uu1 = LTI ? u1v : u1v + V1(k);
                 J += R0 * uu0 * uu0 + R1 * uu1 * uu1;
                 uint32_t hk = Hf.get(k);
                 const T px = PX(k), py = PY(k);
@@ -363,11 +416,18 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                     }
                 }
                 Hf.set(k, hk);
-                const T vr = fabs(V0[k]) > (T)0.01 ? V0[k] : (T)0.1;
-                const T n0 = x0 + (-vr * S[k] * dt) * x2 + (Cs[k] * dt) * u0v;
-                const T n1 = x1 + (vr * Cs[k] * dt) * x2 + (S[k] * dt) * u0v;
-                const T n2 = x2 + dt * u1v;
-                x0 = n0; x1 = n1; x2 = n2;
+                if constexpr (LTI) {
+                    const T n0 = x0 + la0 * x2 + lb0 * u0v + S[k];
+                    const T n1 = x1 + la1 * x2 + lb1 * u0v + Cs[k];
+                    const T n2 = x2 + dt * u1v + V0[k];
+                    x0 = n0; x1 = n1; x2 = n2;
+                } else {
+                    const T vr = fabs(V0[k]) > (T)0.01 ? V0[k] : (T)0.1;
+                    const T n0 = x0 + (-vr * S[k] * dt) * x2 + (Cs[k] * dt) * u0v;
+                    const T n1 = x1 + (vr * Cs[k] * dt) * x2 + (S[k] * dt) * u0v;
+                    const T n2 = x2 + dt * u1v;
+                    x0 = n0; x1 = n1; x2 = n2;
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -417,7 +477,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     // ---- outputs (mpc_controller.py:484-520): x_pred = x_refs + dx (not unwrapped),
     // u = u_refs + du, omega ramp, step counter.  In fp32 the fp64 references are re-read so
     // that only the deviations carry fp32 rounding.
-    const int sc = a.step_count ? a.step_count[b] : 0;
+    // LTI: u = du (no u_ref), x_pred = e + x_ref (absolute), no ramp or step count.
+    const int sc = (!LTI && a.step_count) ? a.step_count[b] : 0;
     T x0 = d0, x1 = d1, x2 = d2;
     double uc0 = 0, uc1 = 0;
 #pragma unroll
@@ -430,12 +491,16 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             T g[8];
             gt.ld(j, g);
             T lo0 = -BIG, hi0 = BIG, lo1 = -BIG, hi1 = BIG;
+            if constexpr (LTI) {
+                lo0 = -vmax; hi0 = vmax; lo1 = -omax; hi1 = omax;
+            } else {
 #pragma unroll
-            for (int k = k0; k < k1; k++) {
-                lo0 = fmax(lo0, -vmax - V0[k]);
-                hi0 = fmin(hi0, vmax - V0[k]);
-                lo1 = fmax(lo1, -omax - V1(k));
-                hi1 = fmin(hi1, omax - V1(k));
+                for (int k = k0; k < k1; k++) {
+                    lo0 = fmax(lo0, -vmax - V0[k]);
+                    hi0 = fmin(hi0, vmax - V0[k]);
+                    lo1 = fmax(lo1, -omax - V1(k));
+                    hi1 = fmin(hi1, omax - V1(k));
+                }
             }
             const T e0 = g[0] * x0 + g[1] * x1 + g[2] * x2 + g[6];
             const T e1 = g[3] * x0 + g[4] * x1 + g[5] * x2 + g[7];
@@ -446,10 +511,10 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         }
 #pragma unroll
         for (int k = k0; k < k1; k++) {
-            double v0 = F64 ? (double)(du0 + V0[k]) : (double)du0 + ur[2 * k];
-            double v1 = F64 ? (double)(du1 + V1(k)) : (double)du1 + ur[2 * k + 1];
+            double v0 = LTI ? (double)du0 : F64 ? (double)(du0 + V0[k]) : (double)du0 + ur[2 * k];
+            double v1 = LTI ? (double)du1 : F64 ? (double)(du1 + V1(k)) : (double)du1 + ur[2 * k + 1];
             if (k == 0) {
-                if (sc < p.ramp_up_steps) {                           // :502-505
+                if (!LTI && sc < p.ramp_up_steps) {                   // :502-505 (LTV only)
                     const double lim = p.omega_max * ((double)(sc + 1) / (double)p.ramp_up_steps);
                     v1 = clampv(v1, -lim, lim);
                 }
@@ -462,24 +527,39 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             }
             if (a.x_pred) {
                 double *xp = a.x_pred + ((size_t)b * (N + 1) + k) * 3;
-                xp[0] = F64 ? (double)(x0 + PX(k)) : (double)x0 + xr[3 * k];
-                xp[1] = F64 ? (double)(x1 + PY(k)) : (double)x1 + xr[3 * k + 1];
-                xp[2] = (double)x2 + xr[3 * k + 2];
+                if constexpr (LTI) {
+                    xp[0] = (double)(x0 + PX(k)); xp[1] = (double)(x1 + PY(k)); xp[2] = (double)(x2 + V1(k));
+                } else {
+                    xp[0] = F64 ? (double)(x0 + PX(k)) : (double)x0 + xr[3 * k];
+                    xp[1] = F64 ? (double)(x1 + PY(k)) : (double)x1 + xr[3 * k + 1];
+                    xp[2] = (double)x2 + xr[3 * k + 2];
+                }
             }
-            const T vr = fabs(V0[k]) > (T)0.01 ? V0[k] : (T)0.1;
-            const T n0 = x0 + (-vr * S[k] * dt) * x2 + (Cs[k] * dt) * du0;
-            const T n1 = x1 + (vr * Cs[k] * dt) * x2 + (S[k] * dt) * du0;
-            const T n2 = x2 + dt * du1;
-            x0 = n0; x1 = n1; x2 = n2;
+            if constexpr (LTI) {
+                const T n0 = x0 + la0 * x2 + lb0 * du0 + S[k];
+                const T n1 = x1 + la1 * x2 + lb1 * du0 + Cs[k];
+                const T n2 = x2 + dt * du1 + V0[k];
+                x0 = n0; x1 = n1; x2 = n2;
+            } else {
+                const T vr = fabs(V0[k]) > (T)0.01 ? V0[k] : (T)0.1;
+                const T n0 = x0 + (-vr * S[k] * dt) * x2 + (Cs[k] * dt) * du0;
+                const T n1 = x1 + (vr * Cs[k] * dt) * x2 + (S[k] * dt) * du0;
+                const T n2 = x2 + dt * du1;
+                x0 = n0; x1 = n1; x2 = n2;
+            }
         }
     }
     if (a.x_pred) {
         double *xp = a.x_pred + ((size_t)b * (N + 1) + N) * 3;
-        xp[0] = (double)x0 + xr[3 * N];
-        xp[1] = (double)x1 + xr[3 * N + 1];
-        xp[2] = (double)x2 + xr[3 * N + 2];
+        if constexpr (LTI) {
+            xp[0] = (double)x0 + xsN0; xp[1] = (double)x1 + xsN1; xp[2] = (double)x2 + xsN2;
+        } else {
+            xp[0] = (double)x0 + xr[3 * N];
+            xp[1] = (double)x1 + xr[3 * N + 1];
+            xp[2] = (double)x2 + xr[3 * N + 2];
+        }
     }
-    if (a.step_count) a.step_count[b] = sc + 1;                        // :507
+    if (!LTI && a.step_count) a.step_count[b] = sc + 1;                // :507 (LTV only)
     a.u0[2 * b] = uc0;
     a.u0[2 * b + 1] = uc1;
     if (a.cost) a.cost[b] = (double)J;
@@ -496,25 +576,32 @@ using namespace rmpc;
 #undef PY
 #undef V1
 
-bool rmpc_mpc_fast_supported(int N, int bs, int prec) {
+bool rmpc_mpc_fast_supported(int N, int bs, int prec, bool lti) {
+    if (lti) return prec != RMPC_F32 && (N == 6 || N == 10 || N == 20);   // LTI: block size unused
     if (prec == RMPC_F32) return bs == 1 && (N == 20 || N == 30);
     return (bs == 1 && (N == 6 || N == 10 || N == 20)) || (bs == 2 && N == 6);
 }
 
-hipError_t rmpc_launch_mpc_fast(const MpcFastArgs &a, int N, int bs, int prec, hipStream_t stream) {
+hipError_t rmpc_launch_mpc_fast(const MpcFastArgs &a, int N, int bs, int prec, hipStream_t stream, bool lti) {
     const int64_t n = a.B;
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + RMPC_WAVE - 1) / RMPC_WAVE)), block(RMPC_WAVE);
     const size_t lds = (size_t)3 * N * RMPC_WAVE * (prec == RMPC_F32 ? sizeof(float) : sizeof(double));
-    if (prec == RMPC_F32) {
-        if (bs == 1 && N == 30) hipLaunchKernelGGL((mpc_ltv_fast_kernel<30, 1, float>), grid, block, lds, stream, a);
-        else if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, float>), grid, block, lds, stream, a);
+    if (lti) {
+        if (prec == RMPC_F32) return hipErrorInvalidValue;
+        if (N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, true>), grid, block, lds, stream, a);
+        else if (N == 10) hipLaunchKernelGGL((mpc_ltv_fast_kernel<10, 1, double, true>), grid, block, lds, stream, a);
+        else if (N == 6) hipLaunchKernelGGL((mpc_ltv_fast_kernel<6, 1, double, true>), grid, block, lds, stream, a);
+        else return hipErrorInvalidValue;
+    } else if (prec == RMPC_F32) {
+        if (bs == 1 && N == 30) hipLaunchKernelGGL((mpc_ltv_fast_kernel<30, 1, float, false>), grid, block, lds, stream, a);
+        else if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, float, false>), grid, block, lds, stream, a);
         else return hipErrorInvalidValue;
     } else {
-        if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double>), grid, block, lds, stream, a);
-        else if (bs == 1 && N == 10) hipLaunchKernelGGL((mpc_ltv_fast_kernel<10, 1, double>), grid, block, lds, stream, a);
-        else if (bs == 1 && N == 6) hipLaunchKernelGGL((mpc_ltv_fast_kernel<6, 1, double>), grid, block, lds, stream, a);
-        else if (bs == 2 && N == 6) hipLaunchKernelGGL((mpc_ltv_fast_kernel<6, 2, double>), grid, block, lds, stream, a);
+        if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, false>), grid, block, lds, stream, a);
+        else if (bs == 1 && N == 10) hipLaunchKernelGGL((mpc_ltv_fast_kernel<10, 1, double, false>), grid, block, lds, stream, a);
+        else if (bs == 1 && N == 6) hipLaunchKernelGGL((mpc_ltv_fast_kernel<6, 1, double, false>), grid, block, lds, stream, a);
+        else if (bs == 2 && N == 6) hipLaunchKernelGGL((mpc_ltv_fast_kernel<6, 2, double, false>), grid, block, lds, stream, a);
         else return hipErrorInvalidValue;
     }
     return hipGetLastError();
