@@ -29,6 +29,11 @@
 #include <cstdio>
 #include <cstdlib>
 
+// 1: rollouts and adjoints of given inputs by group scans (default); 0: sequential sweeps
+#ifndef RMPC_GROUP_SCAN
+#define RMPC_GROUP_SCAN 1
+#endif
+
 namespace rmpc {
 
 struct GroupArgs {
@@ -100,18 +105,76 @@ __device__ __forceinline__ bool gany(bool v, int grp) {
     return ((m >> (grp * G)) & ((1ull << G) - 1)) != 0;
 }
 
+// DPP lane move within a row of 16 lanes (lanes whose source is outside the row read 0)
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+    const long long bits = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)bits, CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(bits >> 32), CTRL, 0xF, 0xF, true);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+enum {
+    DPP_QUAD_XOR1 = 0xB1, DPP_QUAD_XOR2 = 0x4E,          // quad_perm [1,0,3,2] / [2,3,0,1]
+    DPP_ROW_SHL = 0x100, DPP_ROW_SHR = 0x110, DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141
+};
+
+// Group reductions.  For G = 16 (one DPP row): quad butterflies, then the half-row and row
+// mirrors.  Every stage adds a lane's value to its partner's and the partner does the same
+// addition the other way round, so all lanes end with bitwise-identical results (the
+// recursions that follow rely on that).  Wider groups use shuffles.
 template <int G, typename V>
 __device__ __forceinline__ V gsum(V v) {
+    if constexpr (G == 16) {
+        v += dpp_mov<DPP_QUAD_XOR1>(v);
+        v += dpp_mov<DPP_QUAD_XOR2>(v);
+        v += dpp_mov<DPP_ROW_HALF_MIRROR>(v);
+        v += dpp_mov<DPP_ROW_MIRROR>(v);
+    } else {
 #pragma unroll
-    for (int off = G / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        for (int off = G / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    }
     return v;
 }
 
 template <int G, typename V>
 __device__ __forceinline__ V gmaxv(V v) {
+    if constexpr (G == 16) {
+        v = fmax(v, dpp_mov<DPP_QUAD_XOR1>(v));
+        v = fmax(v, dpp_mov<DPP_QUAD_XOR2>(v));
+        v = fmax(v, dpp_mov<DPP_ROW_HALF_MIRROR>(v));
+        v = fmax(v, dpp_mov<DPP_ROW_MIRROR>(v));
+    } else {
 #pragma unroll
-    for (int off = G / 2; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+        for (int off = G / 2; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+    }
     return v;
+}
+
+// Exclusive prefix sum over the group's lanes in lane order (FWD) or in reverse lane order
+// (the sum over the lanes above).  G = 16 is one DPP row (Hillis-Steele with row shifts);
+// wider groups go through shuffles.
+template <int G, bool FWD, typename V>
+__device__ __forceinline__ V gscan_excl(V v, int gl) {
+    if constexpr (G == 16) {
+        constexpr int S = FWD ? DPP_ROW_SHR : DPP_ROW_SHL;
+        v += dpp_mov<S + 1>(v);
+        v += dpp_mov<S + 2>(v);
+        v += dpp_mov<S + 4>(v);
+        v += dpp_mov<S + 8>(v);
+        return dpp_mov<S + 1>(v);
+    } else {
+#pragma unroll
+        for (int off = 1; off < G; off <<= 1) {
+            const V t = FWD ? __shfl_up(v, off, G) : __shfl_down(v, off, G);
+            if (FWD ? gl >= off : gl + off < G) v += t;
+        }
+        const V t = FWD ? __shfl_up(v, 1, G) : __shfl_down(v, 1, G);
+        return (FWD ? gl >= 1 : gl + 1 < G) ? t : (V)0;
+    }
 }
 
 enum { PH_PDAS = 0, PH_PN = 1, PH_DONE = 2, PH_IDLE = 3 };
@@ -330,6 +393,77 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         return gsum<G>(jl);
     };
 
+#if RMPC_GROUP_SCAN
+    // Trajectory under given inputs, in parallel over the horizon.  The model is triangular:
+    // theta integrates dt*w, and x, y integrate a_k*theta_k + b_k*v_k.  So the rollout is two
+    // group prefix sums over contiguous chunks of C steps per lane.  Each lane then walks its
+    // chunk, stores its states (XS, lanes of groups with m set) and adds its steps' objective
+    // terms, the same terms as cost().
+    auto objective = [&](int zoff, bool m, int &used) __attribute__((always_inline)) -> T {
+        refresh();
+        constexpr int C = (N + G - 1) / G;
+        const int k0 = gl * C;
+        T w0[C], w1[C], s0[C], s1[C], s2[C], s3[C];
+        T a2 = 0;
+#pragma unroll
+        for (int i = 0; i < C; i++) {
+            const int k = k0 + i;
+            const bool in = k < N;
+            const int kk = in ? k : 0;
+            w0[i] = in ? base[zoff + 2 * (kk / BS)] : (T)0;
+            w1[i] = in ? base[zoff + 2 * (kk / BS) + 1] : (T)0;
+            s0[i] = STG(0, kk); s1[i] = STG(1, kk); s2[i] = STG(2, kk); s3[i] = STG(3, kk);
+            a2 += dt * w1[i];
+        }
+        T th = d2 + gscan_excl<G, true>(a2, gl);
+        T thc[C], a0 = 0, a1 = 0;
+#pragma unroll
+        for (int i = 0; i < C; i++) {
+            thc[i] = th;
+            if (k0 + i < N) {
+                a0 += s0[i] * th + s2[i] * w0[i];
+                a1 += s1[i] * th + s3[i] * w0[i];
+                th += dt * w1[i];
+            }
+        }
+        T px = d0 + gscan_excl<G, true>(a0, gl), py = d1 + gscan_excl<G, true>(a1, gl);
+        T *const jk = junk;
+        T jl = 0;
+        int u = 0;
+#pragma unroll
+        for (int i = 0; i < C; i++) {
+            const int k = k0 + i;
+            if (k < N) {
+                *(m ? &XS(k, 0) : jk) = px;
+                *(m ? &XS(k, 1) : jk) = py;
+                *(m ? &XS(k, 2) : jk) = thc[i];
+                const T e0 = LTI ? px - XR(k, 0) : px, e1 = LTI ? py - XR(k, 1) : py;
+                const T e2 = LTI ? thc[i] - XR(k, 2) : thc[i];
+                jl += Q0 * e0 * e0 + Q1 * e1 * e1 + Q2 * e2 * e2;
+                const T uu0 = w0[i] + STG(4, k), uu1 = w1[i] + STG(5, k);
+                jl += R0 * uu0 * uu0 + R1 * uu1 * uu1;
+                for (int o = 0; o < no; o++) {
+                    const T r = HB(o, k) - HN0(o, k) * px - HN1(o, k) * py;
+                    if (r > 0) jl += rho * r * r;
+                    u |= (r > 1e-6);
+                }
+                px += s0[i] * thc[i] + s2[i] * w0[i];
+                py += s1[i] * thc[i] + s3[i] * w0[i];
+            }
+        }
+        if (k0 < N && k0 + C >= N) {          // this lane's chunk ends at the horizon: x_N
+            *(m ? &XS(N, 0) : jk) = px;
+            *(m ? &XS(N, 1) : jk) = py;
+            *(m ? &XS(N, 2) : jk) = th;
+            const T e0 = LTI ? px - XR(N, 0) : px, e1 = LTI ? py - XR(N, 1) : py;
+            const T e2 = LTI ? th - XR(N, 2) : th;
+            jl += P0 * e0 * e0 + P1 * e1 * e1 + P2 * e2 * e2;
+        }
+        __syncthreads();
+        used = gany<G>(u, grp);
+        return gsum<G>(jl);
+    };
+#else
     auto objective = [&](int zoff, bool m, int &used) __attribute__((always_inline)) -> T {
         refresh();
         T x0 = d0, x1 = d1, x2 = d2;
@@ -359,6 +493,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         __syncthreads();
         return cost(zoff, used);
     };
+#endif
 
     // the quadratic piece of the current sets (HF, BF; fixed components at their bounds):
     // backward Riccati sweep -> GN; forward sweep -> candidate ZC, trajectory XS, next box
@@ -519,7 +654,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
 
     // gradient of the objective at ZZ (whose trajectory is in XS): hinge forces per step
     // (lane-parallel), then the adjoint recursion (uniform) -> GR
-    auto gradient = [&](bool m) __attribute__((always_inline)) {
+    auto gradient_seq = [&](bool m) __attribute__((always_inline)) {
         refresh();
         for (int k = gl; k < N; k += G) {
             T f0 = 0.0, f1 = 0.0;
@@ -557,6 +692,78 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         }
         __syncthreads();
     };
+
+#if RMPC_GROUP_SCAN
+    // The adjoint is a pair of suffix sums too: lambda_{x,y} accumulate 2Q e + hinge forces,
+    // and lambda_theta accumulates 2Q e_theta + a_k . lambda_{x,y}(k+1).  Two reverse group
+    // scans over the same chunks, then each lane forms its steps' gradient (BS = 1).
+    auto gradient = [&](bool m) __attribute__((always_inline)) {
+        if constexpr (BS == 1) {
+            refresh();
+            constexpr int C = (N + G - 1) / G;
+            const int k0 = gl * C;
+            T c0[C], c1[C], c2[C];
+            T A0 = 0, A1 = 0;
+#pragma unroll
+            for (int i = 0; i < C; i++) {
+                const int k = k0 + i;
+                c0[i] = 0; c1[i] = 0; c2[i] = 0;
+                if (k < N) {
+                    const T y0 = XS(k, 0), y1 = XS(k, 1), y2 = XS(k, 2);
+                    T f0 = 0, f1 = 0;
+                    if (k > 0) {
+                        for (int o = 0; o < no; o++) {
+                            const T r = HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1;
+                            if (r > 0) {
+                                f0 -= 2 * rho * r * HN0(o, k);
+                                f1 -= 2 * rho * r * HN1(o, k);
+                            }
+                        }
+                    }
+                    c0[i] = 2 * Q0 * (LTI ? y0 - XR(k, 0) : y0) + f0;
+                    c1[i] = 2 * Q1 * (LTI ? y1 - XR(k, 1) : y1) + f1;
+                    c2[i] = 2 * Q2 * (LTI ? y2 - XR(k, 2) : y2);
+                    A0 += c0[i];
+                    A1 += c1[i];
+                }
+            }
+            const T t0 = 2 * P0 * (LTI ? XS(N, 0) - XR(N, 0) : XS(N, 0));
+            const T t1 = 2 * P1 * (LTI ? XS(N, 1) - XR(N, 1) : XS(N, 1));
+            const T t2 = 2 * P2 * (LTI ? XS(N, 2) - XR(N, 2) : XS(N, 2));
+            T L0 = t0 + gscan_excl<G, false>(A0, gl), L1 = t1 + gscan_excl<G, false>(A1, gl);
+            T l0n[C], l1n[C], A2 = 0;
+#pragma unroll
+            for (int i = C - 1; i >= 0; i--) {
+                const int k = k0 + i;
+                l0n[i] = L0; l1n[i] = L1;
+                if (k < N) {
+                    c2[i] += STG(0, k) * L0 + STG(1, k) * L1;
+                    A2 += c2[i];
+                    L0 += c0[i];
+                    L1 += c1[i];
+                }
+            }
+            T L2 = t2 + gscan_excl<G, false>(A2, gl);
+            T *const jk = junk;
+#pragma unroll
+            for (int i = C - 1; i >= 0; i--) {
+                const int k = k0 + i;
+                if (k < N) {
+                    const T g0 = STG(2, k) * l0n[i] + STG(3, k) * l1n[i] + 2 * R0 * (ZZ(2 * k) + STG(4, k));
+                    const T g1 = dt * L2 + 2 * R1 * (ZZ(2 * k + 1) + STG(5, k));
+                    *(m ? &GR(2 * k) : jk) = g0;
+                    *(m ? &GR(2 * k + 1) : jk) = g1;
+                    L2 += c2[i];
+                }
+            }
+            __syncthreads();
+        } else {
+            gradient_seq(m);
+        }
+    };
+#else
+    auto gradient = [&](bool m) __attribute__((always_inline)) { gradient_seq(m); };
+#endif
 
     // ---- the iteration loop (groups in lockstep)
     bool done_ok = false;             // certified with a finite objective: written after the loop

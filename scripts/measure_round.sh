@@ -15,6 +15,8 @@ for c in cfg2 cfg4 cfg5; do
   step bench $c
   timeout -k 10 300 python bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/${tag}_bench_$c.json 2> gpurun_out/${tag}_bench_$c.err || exit $?
 done
+step bench lti
+timeout -k 10 300 python bench.py --lti --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/${tag}_bench_lti.json 2> gpurun_out/${tag}_bench_lti.err || exit $?
 step rocprof
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/${tag}_prof_bench.json 2> gpurun_out/${tag}_prof.err || exit $?
 step done
