@@ -154,6 +154,42 @@ __device__ __forceinline__ V gmaxv(V v) {
     return v;
 }
 
+// The value of the lane OFF below in the group (0 for the group's first OFF lanes)
+template <int G, int OFF, typename V>
+__device__ __forceinline__ V gshr(V v, int gl) {
+    if constexpr (G == 16) {
+        return dpp_mov<DPP_ROW_SHR + OFF>(v);
+    } else {
+        const V t = __shfl_up(v, OFF, G);
+        return gl >= OFF ? t : (V)0;
+    }
+}
+
+// One Hillis-Steele stage of an inclusive scan of affine maps x -> F x + f (3x3, lane
+// order = step order): lanes at or above OFF compose their map after the one OFF below.
+template <int G, int OFF, typename V>
+__device__ __forceinline__ void affine_scan_stage(V F[9], V f[3], int gl) {
+    V P[9], p[3];
+#pragma unroll
+    for (int i = 0; i < 9; i++) P[i] = gshr<G, OFF>(F[i], gl);
+#pragma unroll
+    for (int i = 0; i < 3; i++) p[i] = gshr<G, OFF>(f[i], gl);
+    if (gl >= OFF) {
+        V nF[9], nf[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+                nF[3 * r + c] = F[3 * r] * P[c] + F[3 * r + 1] * P[3 + c] + F[3 * r + 2] * P[6 + c];
+            nf[r] = F[3 * r] * p[0] + F[3 * r + 1] * p[1] + F[3 * r + 2] * p[2] + f[r];
+        }
+#pragma unroll
+        for (int i = 0; i < 9; i++) F[i] = nF[i];
+#pragma unroll
+        for (int i = 0; i < 3; i++) f[i] = nf[i];
+    }
+}
+
 // Exclusive prefix sum over the group's lanes in lane order (FWD) or in reverse lane order
 // (the sum over the lanes above).  G = 16 is one DPP row (Hillis-Steele with row shifts);
 // wider groups go through shuffles.
@@ -291,7 +327,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         // linearisation and the hinge rows of this lane's steps, the blocked box per block
         double thl[KPL];
         double corr = 0.0, prev = xr[2], th0 = 0.0;
-    #pragma unroll
+#pragma unroll
         for (int k = 0; k < N; k++) {
             const double th = xr[3 * k + 2];
             if (k > 0) corr += unwrap_step(prev, th);
@@ -300,7 +336,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
             if (k == 0) th0 = thu;
             if (k % G == gl) thl[k / G] = thu;
         }
-    #pragma unroll
+#pragma unroll
         for (int i = 0; i < KPL; i++) {
             const int k = gl + G * i;
             if (k < N) {
@@ -399,19 +435,16 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
     // group prefix sums over contiguous chunks of C steps per lane.  Each lane then walks its
     // chunk, stores its states (XS, lanes of groups with m set) and adds its steps' objective
     // terms, the same terms as cost().
-    auto objective = [&](int zoff, bool m, int &used) __attribute__((always_inline)) -> T {
-        refresh();
-        constexpr int C = (N + G - 1) / G;
+    constexpr int CH = (N + G - 1) / G;      // steps per lane in the scan layouts
+    auto rollout_cost = [&](const T (&w0)[CH], const T (&w1)[CH], bool m, int &used) __attribute__((always_inline)) -> T {
+        constexpr int C = CH;
         const int k0 = gl * C;
-        T w0[C], w1[C], s0[C], s1[C], s2[C], s3[C];
+        T s0[C], s1[C], s2[C], s3[C];
         T a2 = 0;
 #pragma unroll
         for (int i = 0; i < C; i++) {
             const int k = k0 + i;
-            const bool in = k < N;
-            const int kk = in ? k : 0;
-            w0[i] = in ? base[zoff + 2 * (kk / BS)] : (T)0;
-            w1[i] = in ? base[zoff + 2 * (kk / BS) + 1] : (T)0;
+            const int kk = k < N ? k : 0;
             s0[i] = STG(0, kk); s1[i] = STG(1, kk); s2[i] = STG(2, kk); s3[i] = STG(3, kk);
             a2 += dt * w1[i];
         }
@@ -459,9 +492,56 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
             const T e2 = LTI ? th - XR(N, 2) : th;
             jl += P0 * e0 * e0 + P1 * e1 * e1 + P2 * e2 * e2;
         }
-        __syncthreads();
         used = gany<G>(u, grp);
         return gsum<G>(jl);
+    };
+    auto objective = [&](int zoff, bool m, int &used) __attribute__((always_inline)) -> T {
+        refresh();
+        const int k0 = gl * CH;
+        T w0[CH], w1[CH];
+#pragma unroll
+        for (int i = 0; i < CH; i++) {
+            const int k = k0 + i;
+            const bool in = k < N;
+            const int kk = in ? k : 0;
+            w0[i] = in ? base[zoff + 2 * (kk / BS)] : (T)0;
+            w1[i] = in ? base[zoff + 2 * (kk / BS) + 1] : (T)0;
+        }
+        const T J = rollout_cost(w0, w1, m, used);
+        __syncthreads();
+        return J;
+    };
+    // One Armijo trial of the projected-Newton search (BS = 1), fused: each lane forms its
+    // steps' trial inputs z_t = clamp(z + alpha (z_c - z)) and their gradient term, rolls
+    // out and costs them, and -- when the group accepts -- writes them to ZZ itself.
+    auto ls_trial = [&](T alpha, bool m, T Fc, bool &acc) __attribute__((always_inline)) -> T {
+        refresh();
+        const int k0 = gl * CH;
+        T w0[CH], w1[CH], gd = 0;
+#pragma unroll
+        for (int i = 0; i < CH; i++) {
+            const int k = k0 + i;
+            w0[i] = 0; w1[i] = 0;
+            if (k < N) {
+                const T z0 = ZZ(2 * k), z1 = ZZ(2 * k + 1);
+                w0[i] = clampv(z0 + alpha * (ZC(2 * k) - z0), BND(0, k), BND(1, k));
+                w1[i] = clampv(z1 + alpha * (ZC(2 * k + 1) - z1), BND(2, k), BND(3, k));
+                gd += GR(2 * k) * (w0[i] - z0) + GR(2 * k + 1) * (w1[i] - z1);
+            }
+        }
+        int u;
+        const T Ft = rollout_cost(w0, w1, m, u);
+        gd = gsum<G>(gd);
+        acc = m && Ft <= Fc + (T)1e-4 * gd;
+        if (acc) {
+#pragma unroll
+            for (int i = 0; i < CH; i++) {
+                const int k = k0 + i;
+                if (k < N) { ZZ(2 * k) = w0[i]; ZZ(2 * k + 1) = w1[i]; }
+            }
+        }
+        __syncthreads();
+        return Ft;
     };
 #else
     auto objective = [&](int zoff, bool m, int &used) __attribute__((always_inline)) -> T {
@@ -492,6 +572,115 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         GSTM(XS(N, 0), x0, m); GSTM(XS(N, 1), x1, m); GSTM(XS(N, 2), x2, m);
         __syncthreads();
         return cost(zoff, used);
+    };
+#endif
+
+    // PDAS hinge rule of step k's rows at position (y0, y1): the next flags from the current h
+    auto hinge_rule = [&](int k, uint32_t h, T y0, T y1) __attribute__((always_inline)) -> uint32_t {
+        uint32_t nh = h;
+        if (k > 0) {
+            for (int o = 0; o < no; o++) {
+                const T r = HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1;
+                const uint32_t act = (h >> o) & 1u;
+                const uint32_t na = act ? (r > -eps_h) : (r > eps_h);
+                nh ^= (na ^ act) << o;
+            }
+        }
+        return nh;
+    };
+
+#if RMPC_GROUP_SCAN
+    // Forward sweep of solve_test in parallel over the horizon (BS = 1).  With the box states
+    // fixed, step k is the affine map x -> M_k x + m_k: a free input follows its gain row, a
+    // fixed one sits at its bound.  Each lane composes the maps of its chunk of C steps, a
+    // group scan of the composites gives every chunk's start state, and each lane then walks
+    // its chunk with the step formulas of the sequential sweep (inputs, box rule, trajectory)
+    // and applies the hinge rule to its steps' rows.
+    auto forward_scan = [&](bool &bchg, bool &hchg) __attribute__((always_inline)) {
+        constexpr int C = (N + G - 1) / G;
+        const int k0 = gl * C;
+        T rc[C][16];
+        uint32_t rb[C];
+        T F[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, f[3] = {0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < C; i++) {
+            const int k = k0 + i;
+            const int kk = k < N ? k : N - 1;
+#pragma unroll
+            for (int q = 0; q < 12; q++) rc[i][q] = base[RC::BLK + 12 * kk + q];
+#pragma unroll
+            for (int q = 0; q < 4; q++) rc[i][12 + q] = base[RC::STEP + 12 * kk + q];
+            rb[i] = BF(kk);
+            if (k < N) {
+                T c[16];
+#pragma unroll
+                for (int q = 0; q < 16; q++) c[q] = rc[i][q];
+                const int bf0 = rb[i] & 3, bf1 = (rb[i] >> 2) & 3;
+                const bool fr0 = bf0 == 0, fr1 = bf1 == 0;
+                const T g00 = fr0 ? c[4] : (T)0, g01 = fr0 ? c[5] : (T)0, g02 = fr0 ? c[6] : (T)0;
+                const T g10 = fr1 ? c[7] : (T)0, g11 = fr1 ? c[8] : (T)0, g12 = fr1 ? c[9] : (T)0;
+                const T kp0 = fr0 ? c[10] : (bf0 == 1 ? c[0] : c[1]);
+                const T kp1 = fr1 ? c[11] : (bf1 == 1 ? c[2] : c[3]);
+                const T sa0 = c[12], sa1 = c[13], sb0 = c[14], sb1 = c[15];
+                const T M[9] = {(T)1 + sb0 * g00, sb0 * g01, sa0 + sb0 * g02,
+                                sb1 * g00, (T)1 + sb1 * g01, sa1 + sb1 * g02,
+                                dt * g10, dt * g11, (T)1 + dt * g12};
+                const T m[3] = {sb0 * kp0, sb1 * kp0, dt * kp1};
+                T nF[9], nf[3];
+#pragma unroll
+                for (int r = 0; r < 3; r++) {
+#pragma unroll
+                    for (int cc = 0; cc < 3; cc++)
+                        nF[3 * r + cc] = M[3 * r] * F[cc] + M[3 * r + 1] * F[3 + cc] + M[3 * r + 2] * F[6 + cc];
+                    nf[r] = M[3 * r] * f[0] + M[3 * r + 1] * f[1] + M[3 * r + 2] * f[2] + m[r];
+                }
+#pragma unroll
+                for (int q = 0; q < 9; q++) F[q] = nF[q];
+#pragma unroll
+                for (int q = 0; q < 3; q++) f[q] = nf[q];
+            }
+        }
+        affine_scan_stage<G, 1>(F, f, gl);
+        affine_scan_stage<G, 2>(F, f, gl);
+        affine_scan_stage<G, 4>(F, f, gl);
+        affine_scan_stage<G, 8>(F, f, gl);
+        if constexpr (G >= 32) affine_scan_stage<G, 16>(F, f, gl);
+        if constexpr (G >= 64) affine_scan_stage<G, 32>(F, f, gl);
+        // the state after this lane's chunk, one lane up: the chunk's start state
+        const T y0 = F[0] * d0 + F[1] * d1 + F[2] * d2 + f[0];
+        const T y1 = F[3] * d0 + F[4] * d1 + F[5] * d2 + f[1];
+        const T y2 = F[6] * d0 + F[7] * d1 + F[8] * d2 + f[2];
+        T x0 = gshr<G, 1>(y0, gl), x1 = gshr<G, 1>(y1, gl), x2 = gshr<G, 1>(y2, gl);
+        if (gl == 0) { x0 = d0; x1 = d1; x2 = d2; }
+#pragma unroll
+        for (int i = 0; i < C; i++) {
+            const int k = k0 + i;
+            if (k < N) {
+                T c[16];
+#pragma unroll
+                for (int q = 0; q < 16; q++) c[q] = rc[i][q];
+                const T lo0 = c[0], hi0 = c[1], lo1 = c[2], hi1 = c[3];
+                const T e0 = c[4] * x0 + c[5] * x1 + c[6] * x2 + c[10];
+                const T e1 = c[7] * x0 + c[8] * x1 + c[9] * x2 + c[11];
+                const int bf0 = rb[i] & 3, bf1 = (rb[i] >> 2) & 3;
+                const T u0v = bf0 == 0 ? e0 : (bf0 == 1 ? lo0 : hi0);
+                const T u1v = bf1 == 0 ? e1 : (bf1 == 1 ? lo1 : hi1);
+                const int ns0 = box_rule_bf(bf0, e0, lo0, hi0, eps_b), ns1 = box_rule_bf(bf1, e1, lo1, hi1, eps_b);
+                bchg = bchg || ns0 != bf0 || ns1 != bf1;
+                NBF(k) = (uint32_t)(ns0 | (ns1 << 2));
+                ZC(2 * k) = u0v;
+                ZC(2 * k + 1) = u1v;
+                XS(k, 0) = x0; XS(k, 1) = x1; XS(k, 2) = x2;
+                const uint32_t h = HF(k), nh = hinge_rule(k, h, x0, x1);
+                NHF(k) = nh;
+                hchg = hchg || nh != h;
+                const T n0 = x0 + c[12] * x2 + c[14] * u0v;
+                const T n1 = x1 + c[13] * x2 + c[15] * u0v;
+                const T n2 = x2 + dt * u1v;
+                x0 = n0; x1 = n1; x2 = n2;
+            }
+        }
+        if (k0 < N && k0 + C >= N) { XS(N, 0) = x0; XS(N, 1) = x1; XS(N, 2) = x2; }
     };
 #endif
 
@@ -582,7 +771,13 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         refresh();
         // forward sweep: inputs (free: gains; fixed: bound), box rule on the value (free) or
         // the multiplier (fixed), trajectory
-        bool bchg = false;
+        bool bchg = false, hchg = false;
+#if RMPC_GROUP_SCAN
+        if constexpr (BS == 1) {
+            forward_scan(bchg, hchg);
+        } else
+#endif
+        {   // sequential sweep (block size > 1)
         T x0 = d0, x1 = d1, x2 = d2;
         // block record (bounds + gains) and step data of block j+1 loaded while j computes
         T nx[16];
@@ -630,21 +825,11 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         GPROF(4);
         refresh();
         // hinge rule per row (lane-parallel over steps)
-        bool hchg = false;
         for (int k = gl; k < N; k += G) {
-            const uint32_t h = HF(k);
-            uint32_t nh = h;
-            if (k > 0) {
-                const T y0 = XS(k, 0), y1 = XS(k, 1);
-                for (int o = 0; o < no; o++) {
-                    const T r = HB(o, k) - HN0(o, k) * y0 - HN1(o, k) * y1;
-                    const uint32_t act = (h >> o) & 1u;
-                    const uint32_t na = act ? (r > -eps_h) : (r > eps_h);
-                    nh ^= (na ^ act) << o;
-                }
-            }
+            const uint32_t h = HF(k), nh = hinge_rule(k, h, XS(k, 0), XS(k, 1));
             NHF(k) = nh;
             hchg = hchg || nh != h;
+        }
         }
         const bool chg = gany<G>(bchg || hchg, grp);
         __syncthreads();
@@ -697,17 +882,21 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
     // The adjoint is a pair of suffix sums too: lambda_{x,y} accumulate 2Q e + hinge forces,
     // and lambda_theta accumulates 2Q e_theta + a_k . lambda_{x,y}(k+1).  Two reverse group
     // scans over the same chunks, then each lane forms its steps' gradient (BS = 1).
-    auto gradient = [&](bool m) __attribute__((always_inline)) {
+    // With `sets`, the same pass also builds the projected-Newton sets of the groups with m:
+    // epsilon-active box components and the hinge rows with r > 0.
+    auto gradient = [&](bool m, bool sets) __attribute__((always_inline)) {
         if constexpr (BS == 1) {
             refresh();
             constexpr int C = (N + G - 1) / G;
             const int k0 = gl * C;
             T c0[C], c1[C], c2[C];
+            uint32_t nhb[C];
             T A0 = 0, A1 = 0;
 #pragma unroll
             for (int i = 0; i < C; i++) {
                 const int k = k0 + i;
                 c0[i] = 0; c1[i] = 0; c2[i] = 0;
+                nhb[i] = 0;
                 if (k < N) {
                     const T y0 = XS(k, 0), y1 = XS(k, 1), y2 = XS(k, 2);
                     T f0 = 0, f1 = 0;
@@ -717,6 +906,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
                             if (r > 0) {
                                 f0 -= 2 * rho * r * HN0(o, k);
                                 f1 -= 2 * rho * r * HN1(o, k);
+                                nhb[i] |= 1u << o;
                             }
                         }
                     }
@@ -745,15 +935,44 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
             }
             T L2 = t2 + gscan_excl<G, false>(A2, gl);
             T *const jk = junk;
+            T gz[C][2], zz[C][2], wl = 0;
 #pragma unroll
             for (int i = C - 1; i >= 0; i--) {
                 const int k = k0 + i;
+                gz[i][0] = 0; gz[i][1] = 0; zz[i][0] = 0; zz[i][1] = 0;
                 if (k < N) {
-                    const T g0 = STG(2, k) * l0n[i] + STG(3, k) * l1n[i] + 2 * R0 * (ZZ(2 * k) + STG(4, k));
-                    const T g1 = dt * L2 + 2 * R1 * (ZZ(2 * k + 1) + STG(5, k));
+                    zz[i][0] = ZZ(2 * k); zz[i][1] = ZZ(2 * k + 1);
+                    const T g0 = STG(2, k) * l0n[i] + STG(3, k) * l1n[i] + 2 * R0 * (zz[i][0] + STG(4, k));
+                    const T g1 = dt * L2 + 2 * R1 * (zz[i][1] + STG(5, k));
                     *(m ? &GR(2 * k) : jk) = g0;
                     *(m ? &GR(2 * k + 1) : jk) = g1;
+                    gz[i][0] = g0; gz[i][1] = g1;
                     L2 += c2[i];
+                    if (sets) {
+#pragma unroll
+                        for (int c = 0; c < 2; c++) {
+                            const T lo = BND(2 * c, k), hi = BND(2 * c + 1, k);
+                            wl = fmax(wl, fabs(zz[i][c] - clampv(zz[i][c] - gz[i][c], lo, hi)));
+                        }
+                    }
+                }
+            }
+            if (sets) {
+                const T eps = fmin(SetTol<T>::pn, gmaxv<G>(wl));
+#pragma unroll
+                for (int i = 0; i < C; i++) {
+                    const int k = k0 + i;
+                    if (k < N && m) {
+                        uint32_t w = 0;
+#pragma unroll
+                        for (int c = 0; c < 2; c++) {
+                            const T lo = BND(2 * c, k), hi = BND(2 * c + 1, k), z = zz[i][c], g = gz[i][c];
+                            const uint32_t st = (z <= lo + eps && g > 0) ? 1u : ((z >= hi - eps && g < 0) ? 2u : 0u);
+                            w |= st << (2 * c);
+                        }
+                        BF(k) = w;
+                        HF(k) = nhb[i];
+                    }
                 }
             }
             __syncthreads();
@@ -762,7 +981,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         }
     };
 #else
-    auto gradient = [&](bool m) __attribute__((always_inline)) { gradient_seq(m); };
+    auto gradient = [&](bool m, bool) __attribute__((always_inline)) { gradient_seq(m); };
 #endif
 
     // ---- the iteration loop (groups in lockstep)
@@ -779,7 +998,13 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         if (__any(pn)) {
             // projected Newton: gradient at z, epsilon-active box components, hinge rows with
             // r > 0 -- the sets of this solve (rmpc_mpc_dense.hip phase 2)
-            gradient(pn);
+#if RMPC_GROUP_SCAN
+            if constexpr (BS == 1) {
+                gradient(pn, true);
+            } else
+#endif
+            {
+            gradient(pn, false);
             refresh();
             T wl = 0.0;
             for (int i = gl; i < 2 * NB; i += G) {
@@ -810,6 +1035,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
                 }
             }
             __syncthreads();
+            }
             GPROF(1);
         }
         if (act) it++;
@@ -878,6 +1104,18 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
             refresh();
             T alpha = 1.0;
             for (int ls = 0; ls < 40 && __any(searching); ls++) {
+#if RMPC_GROUP_SCAN
+                if constexpr (BS == 1) {
+                    bool acc;
+                    const T Ft = ls_trial(alpha, searching, F, acc);
+                    if (acc) {
+                        F = Ft;
+                        searching = false;
+                    }
+                    alpha *= (T)0.5;
+                    continue;
+                }
+#endif
                 T gd = 0.0;
                 for (int i = gl; i < 2 * NB; i += G) {
                     const int j = i >> 1, c = i & 1;
