@@ -394,9 +394,13 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                 for (int q = 0; q < 32; q++) fprintf(stderr, " %llu", h[24 + q]);
                 fprintf(stderr, "\n");
                 const double w = h[20] ? (double)h[20] : 1.0;
-                fprintf(stderr, "[fast] waves=%llu per wave: total %.0f back %.0f fwd %.0f iters %.2f | per iter: back %.0f fwd %.0f\n",
+                fprintf(stderr, "[fast] waves=%llu per wave: total %.0f back %.0f fwd %.0f iters %.2f | per iter: back %.0f fwd %.0f"
+                        " | slowest wave: total %llu iters %llu back %llu%%\n",
                         h[20], h[19] / w, h[16] / w, h[17] / w, h[18] / w, h[16] / (double)(h[18] ? h[18] : 1),
-                        h[17] / (double)(h[18] ? h[18] : 1));
+                        h[17] / (double)(h[18] ? h[18] : 1), h[21] >> 16, (h[21] >> 8) & 0xff, h[21] & 0xff);
+                fprintf(stderr, "[fast] waves by loop count 0..7+:");
+                for (int q = 56; q < 64; q++) fprintf(stderr, " %llu", h[q]);
+                fprintf(stderr, "\n");
             }
             dbg_sync(s, "group");
             left = (const int32_t *)c->retry2.p;

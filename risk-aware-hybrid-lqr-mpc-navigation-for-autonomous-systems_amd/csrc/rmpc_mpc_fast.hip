@@ -455,8 +455,13 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             atomicAdd(a.prof + 16, mb);
             atomicAdd(a.prof + 17, mf);
             atomicAdd(a.prof + 18, mi);
-            atomicAdd(a.prof + 19, __builtin_amdgcn_s_memtime() - tp_setup);
+            const unsigned long long tw = __builtin_amdgcn_s_memtime() - tp_setup;
+            atomicAdd(a.prof + 19, tw);
             atomicAdd(a.prof + 20, 1ull);
+            // slowest wave: total cycles (high bits) | its loop iterations | backward share (%)
+            const unsigned long long pb = mb * 100ull / (tw ? tw : 1ull);
+            atomicMax(a.prof + 21, (tw << 16) | (mi << 8) | (pb & 0xffull));
+            atomicAdd(a.prof + 56 + (mi < 7ull ? mi : 7ull), 1ull);     // waves per loop count
         }
     }
     if (!cert || !isfinite(J)) {
