@@ -105,7 +105,10 @@ typedef struct RmpcRiskParams {
     double d_safe, d_trigger, alpha, beta;          /* risk_metrics.py:51-82 (alpha, beta raw) */
     double threshold_low, threshold_medium, threshold_high;
     int32_t min_dwell_steps;                         /* run_simulation.py:520 (10)  */
-    int32_t _pad0;
+    int32_t use_predicted;  /* 0: the reference's switch (no predicted states, :525-531).
+                               1 (rmpc_rollout_batch, hybrid mode): a robot whose previous step
+                               ran MPC passes that solve's x_pred as predicted_states to
+                               assess_risk (compute_predictive_risk, risk_metrics.py:131-171) */
 } RmpcRiskParams;
 
 /* Per-robot LQR gain cache (lqr_controller.py:84-90): K (6), last (v_r, theta_r), valid flag */

@@ -54,7 +54,7 @@ def mpc_closed_loop(duration=20.0, dt=0.02, obstacles=None, steps=None, mpc_kwar
 
 
 def hybrid_closed_loop(duration=20.0, dt=0.02, obstacles=None, steps=None, mpc_kwargs=None,
-                       lqr_Q=(15.0, 15.0, 8.0), start=0, x0=None):
+                       lqr_Q=(15.0, 15.0, 8.0), start=0, x0=None, predictive=False, risk_kwargs=None):
     g = Figure8(2.0, 0.5, dt)
     tab = g.generate(duration)
     lq = LQRController(list(lqr_Q), [0.1, 0.1], dt, 2.0, 3.0)
@@ -63,16 +63,19 @@ def hybrid_closed_loop(duration=20.0, dt=0.02, obstacles=None, steps=None, mpc_k
               v_max=2.0, omega_max=3.0, solver="OSQP")
     kw.update(mpc_kwargs or {})
     c = MPCController(**kw)
-    rm = RiskMetrics(d_safe=0.3, d_trigger=1.0, alpha=0.6, beta=0.4, threshold_low=0.2,
-                     threshold_medium=0.5)
+    rkw = dict(d_safe=0.3, d_trigger=1.0, alpha=0.6, beta=0.4, threshold_low=0.2,
+               threshold_medium=0.5)
+    rkw.update(risk_kwargs or {})
+    rm = RiskMetrics(**rkw)
     obstacles = default_obstacles() if obstacles is None else obstacles
     x = (g.reference_at_index(start)[0] if x0 is None else np.asarray(x0, float)).copy()
     n = len(tab) - 1 if steps is None else steps
     prev, since = None, 0
+    pred = None            # predictive: the last MPC solve's predicted_states (None after LQR)
     st, ct, used = [x.copy()], [], []
     for k in range(n):
         xr, ur = g.reference_at_index(start + k)
-        a = rm.assess(x, obstacles)
+        a = rm.assess(x, obstacles, pred)
         if since >= 10:                                              # :533-537
             use_mpc = a["use_mpc"]
         else:
@@ -85,9 +88,12 @@ def hybrid_closed_loop(duration=20.0, dt=0.02, obstacles=None, steps=None, mpc_k
         prev = cur
         if use_mpc:
             xs, us = g.segment(start + k, c.N + 1)
-            u = c.solve_with_ltv(x, xs, us, obstacles).optimal_control
+            sol = c.solve_with_ltv(x, xs, us, obstacles)
+            u = sol.optimal_control
+            pred = sol.predicted_states if predictive else None
         else:
             u, _ = lq.compute_control_at_operating_point(x, xr, ur)
+            pred = None
         used.append(use_mpc)
         x = simulate_step(x, u, dt, 2.0, 3.0)
         st.append(x.copy())

@@ -78,7 +78,7 @@ struct RmpcCtx {
     DevBuf fast_gains, retry, retry2, retry_count, prof, retry_sets;
     // closed-loop rollout state (rmpc_rollout_batch)
     DevBuf ro_x, ro_xr, ro_ur, ro_u, ro_step, ro_cache, ro_prev, ro_since, ro_status, ro_used,
-        ro_risk, ro_counts, ro_off;
+        ro_risk, ro_counts, ro_off, ro_pred;
     // stage timing of the last MPC launch (rmpc_ctx_set_timing): events before/after
     // the lane-per-robot, wave-per-robot and generic stages
     bool timing = false;
@@ -135,7 +135,7 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     c->retry2.release();
     c->retry_sets.release();
     for (DevBuf *d : {&c->ro_x, &c->ro_xr, &c->ro_ur, &c->ro_u, &c->ro_step, &c->ro_cache, &c->ro_prev,
-                      &c->ro_since, &c->ro_status, &c->ro_used, &c->ro_risk, &c->ro_counts, &c->ro_off})
+                      &c->ro_since, &c->ro_status, &c->ro_used, &c->ro_risk, &c->ro_counts, &c->ro_off, &c->ro_pred})
         d->release();
     c->prof.release();
     c->retry_count.release();
@@ -238,6 +238,7 @@ static RiskDevParams to_dev(const RmpcRiskParams *p) {
     d.th_med = p->threshold_medium;
     d.th_high = p->threshold_high;
     d.min_dwell = p->min_dwell_steps;
+    d.use_pred = p->use_predicted;
     return d;
 }
 
@@ -668,7 +669,7 @@ static int hybrid_step(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams
                        int32_t ref_rows, const double *u_refs, int32_t uref_rows, const double *obstacles,
                        int32_t n_obs, int32_t *prev_ctrl, int32_t *steps_since, int32_t *step_count,
                        RmpcLqrCache *cache, double *u_out, uint8_t *used_mpc, double *risk_out, void *stream,
-                       const int32_t *ref_off) {
+                       const int32_t *ref_off, double *pred = nullptr) {
     if (!c || !rp || !lp) return fail(RMPC_EINVAL, "ctx/params is NULL");
     RC(check_mpc_params(mp, ref_rows, uref_rows, n_obs));
     RC(check_lqr(lp));
@@ -685,8 +686,11 @@ static int hybrid_step(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams
     HIP_TRY(c->hyb_status.ensure((size_t)B * sizeof(int32_t)));
     int32_t *cnt = (int32_t *)c->counts.p;
     HIP_TRY(hipMemsetAsync(cnt, 0, 16, s));
+    // pred [B][N+1][3] (rollouts with use_predicted): read here for the robots whose previous
+    // step ran MPC, then overwritten by this step's MPC branch
     HIP_TRY(rmpc_launch_hybrid_decide(to_dev(rp), B, x, obstacles, n_obs, prev_ctrl, steps_since, used_mpc,
-                                      risk_out, (int32_t *)c->idx_lqr.p, (int32_t *)c->idx_mpc.p, cnt, s));
+                                      risk_out, (int32_t *)c->idx_lqr.p, (int32_t *)c->idx_mpc.p, cnt, s, pred,
+                                      mp->horizon + 1));
     // LQR branch: x_ref / u_ref = row 0 of the segment (get_reference_at_index(k))
     LqrDevParams ld = to_dev(lp);
     ld.ref_off = ref_off;
@@ -695,7 +699,7 @@ static int hybrid_step(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams
                                     cnt, s));
     // MPC branch: solve_with_ltv on the segment; writes u0 straight into u_out
     return launch_mpc(c, mp, B, x, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs, step_count, u_out,
-                      nullptr, nullptr, nullptr, (int32_t *)c->hyb_status.p, nullptr, nullptr,
+                      nullptr, pred, nullptr, (int32_t *)c->hyb_status.p, nullptr, nullptr,
                       (const int32_t *)c->idx_mpc.p, cnt + 1, s, ref_off);
 }
 
@@ -842,6 +846,14 @@ extern "C" int rmpc_rollout_batch_dev(RmpcCtx *c, const RmpcRolloutParams *rp, c
     int32_t *status = (int32_t *)c->ro_status.p;
     RmpcLqrCache *cache = (RmpcLqrCache *)c->ro_cache.p;
     uint8_t *used_now = (uint8_t *)c->ro_used.p;
+    // hybrid with use_predicted: the x_pred of each robot's last MPC solve, and no robot has
+    // one before its first step
+    double *pred = nullptr;
+    if (mode == 2 && kp && kp->use_predicted) {
+        HIP_TRY(c->ro_pred.ensure((size_t)B * (mp->horizon + 1) * 3 * sizeof(double)));
+        pred = (double *)c->ro_pred.p;
+        HIP_TRY(hipMemsetAsync(used_now, 0, (size_t)B, s));
+    }
     unsigned long long *counts = (unsigned long long *)c->ro_counts.p;
     HIP_TRY(hipMemsetAsync(counts, 0, 4 * sizeof(unsigned long long), s));
     HIP_TRY(rmpc_launch_rollout_init(B, start_index, x0, rp->table_len, rp->A, rp->a, rp->dt, x, prev, since,
@@ -869,7 +881,7 @@ extern "C" int rmpc_rollout_batch_dev(RmpcCtx *c, const RmpcRolloutParams *rp, c
             }
         } else {                                           // :525-559
             RC(hybrid_step(c, kp, lp, mp, B, x, xr, rows, ur, rows, obstacles, n_obs, prev, since, step, cache, u,
-                           used_now, (double *)c->ro_risk.p, s, off));
+                           used_now, (double *)c->ro_risk.p, s, off, pred));
             HIP_TRY(rmpc_launch_status_count(B, (const int32_t *)c->hyb_status.p, used_now, counts, s));
         }
         HIP_TRY(rmpc_launch_rollout_plant(B, x, u, rp->dt, rp->v_max, rp->omega_max, rp->plant_method, k,

@@ -117,16 +117,19 @@ hipError_t rmpc_launch_lqr_gain(const LqrDevParams &p, int64_t B, const double *
 struct RiskDevParams {
     double d_safe, d_trigger, alpha, beta, th_low, th_med, th_high;
     int min_dwell;
+    int use_pred;
 };
 
 hipError_t rmpc_launch_risk(const RiskDevParams &p, int64_t B, const double *x, const double *pred,
                             int n_pred, const double *obstacles, int n_obs, double *out,
                             uint8_t *use_mpc, int32_t *level, hipStream_t stream);
+// pred [B][n_pred][3] (nullable): the predicted states of each robot's last MPC solve, used
+// for robots whose used_mpc flag (read before it is overwritten) is set
 hipError_t rmpc_launch_hybrid_decide(const RiskDevParams &p, int64_t B, const double *x,
                                      const double *obstacles, int n_obs, int32_t *prev_ctrl,
                                      int32_t *steps_since, uint8_t *used_mpc, double *risk_out,
                                      int32_t *idx_lqr, int32_t *idx_mpc, int32_t *counts,
-                                     hipStream_t stream);
+                                     hipStream_t stream, const double *pred = nullptr, int n_pred = 0);
 hipError_t rmpc_launch_plant(int64_t B, const double *x, const double *u, double dt, double v_max,
                              double omega_max, int method, double *x_next, hipStream_t stream);
 hipError_t rmpc_launch_figure8_table(int64_t B, const int32_t *start, int32_t k, int rows, int32_t table_len,

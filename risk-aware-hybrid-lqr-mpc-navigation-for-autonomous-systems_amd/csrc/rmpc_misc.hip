@@ -81,7 +81,8 @@ __global__ __launch_bounds__(256) void hybrid_decide_kernel(RiskDevParams p, int
                                                             const double *obs, int no, int32_t *prev_ctrl,
                                                             int32_t *steps_since, uint8_t *used_mpc,
                                                             double *risk_out, int32_t *idx_lqr,
-                                                            int32_t *idx_mpc, int32_t *counts) {
+                                                            int32_t *idx_mpc, int32_t *counts,
+                                                            const double *pred, int n_pred) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     double md;
@@ -89,7 +90,12 @@ __global__ __launch_bounds__(256) void hybrid_decide_kernel(RiskDevParams p, int
     const double dr = no ? distance_risk(p, x[3 * b], x[3 * b + 1], obs, no, &md, &nid) : 0.0;
     double al, be;
     normalise_weights(p, &al, &be);
-    const double c = al * dr + be * 0.0;
+    // the reference's loop passes no predicted states (pr = 0); with use_pred, a robot whose
+    // previous step ran MPC (used_mpc still holds that step's flag here) passes its x_pred
+    const double pr = (pred && p.use_pred && used_mpc[b]) ? predictive_risk(p, pred + (size_t)3 * n_pred * b, n_pred,
+                                                                              obs, no)
+                                                          : 0.0;
+    const double c = al * dr + be * pr;
     const bool rec = c >= p.th_low;
     const int prev = prev_ctrl[b];
     int since = steps_since[b];
@@ -280,10 +286,10 @@ hipError_t rmpc_launch_hybrid_decide(const RiskDevParams &p, int64_t B, const do
                                      const double *obstacles, int n_obs, int32_t *prev_ctrl,
                                      int32_t *steps_since, uint8_t *used_mpc, double *risk_out,
                                      int32_t *idx_lqr, int32_t *idx_mpc, int32_t *counts,
-                                     hipStream_t stream) {
+                                     hipStream_t stream, const double *pred, int n_pred) {
     if (B <= 0) return hipSuccess;
     hipLaunchKernelGGL(hybrid_decide_kernel, dim3(nblk(B, 256)), dim3(256), 0, stream, p, B, x, obstacles,
-                       n_obs, prev_ctrl, steps_since, used_mpc, risk_out, idx_lqr, idx_mpc, counts);
+                       n_obs, prev_ctrl, steps_since, used_mpc, risk_out, idx_lqr, idx_mpc, counts, pred, n_pred);
     return hipGetLastError();
 }
 

@@ -45,7 +45,7 @@ class RiskParams(C.Structure):
     _fields_ = [("d_safe", C.c_double), ("d_trigger", C.c_double), ("alpha", C.c_double),
                 ("beta", C.c_double), ("threshold_low", C.c_double),
                 ("threshold_medium", C.c_double), ("threshold_high", C.c_double),
-                ("min_dwell_steps", C.c_int32), ("_pad0", C.c_int32)]
+                ("min_dwell_steps", C.c_int32), ("use_predicted", C.c_int32)]
 
 
 class RolloutParams(C.Structure):
@@ -199,8 +199,11 @@ def lqr_params(Q, R, dt, v_max, omega_max, max_iter=64, use_cache=True):
 
 
 def risk_params(d_safe=0.3, d_trigger=1.0, alpha=0.6, beta=0.4, threshold_low=0.2,
-                threshold_medium=0.5, threshold_high=0.8, min_dwell_steps=10):
+                threshold_medium=0.5, threshold_high=0.8, min_dwell_steps=10, use_predicted=False):
+    """use_predicted: hybrid rollouts feed each robot's last MPC x_pred to the risk (off in
+    the reference's loop, run_simulation.py:525-531)."""
     p = RiskParams()
+    p.use_predicted = int(bool(use_predicted))
     p.d_safe, p.d_trigger, p.alpha, p.beta = d_safe, d_trigger, alpha, beta
     p.threshold_low, p.threshold_medium, p.threshold_high = (threshold_low, threshold_medium,
                                                              threshold_high)

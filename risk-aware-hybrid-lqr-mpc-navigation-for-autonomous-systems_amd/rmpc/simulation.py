@@ -133,9 +133,15 @@ def run_mpc_simulation(duration=20.0, dt=0.02, with_obstacles=True, scenario="de
 
 
 def run_hybrid_simulation(duration=20.0, dt=0.02, scenario="default", robots=1, start_index=None,
-                          x0=None, horizon=6, block_size=1, device=0, log_dir=None):
+                          x0=None, horizon=6, block_size=1, device=0, log_dir=None,
+                          use_predictive_risk=False):
     """run_simulation.py:413-612 for `robots` robots: risk-threshold switching with a 10-step
-    dwell; risk_history is the combined risk of each step's state (:529)."""
+    dwell; risk_history is the combined risk of each step's state (:529).
+
+    use_predictive_risk=True (not in the reference's loop, which passes no predicted states):
+    a robot whose previous step ran MPC passes that solve's predicted_states to the risk
+    assessment (RiskMetrics.compute_predictive_risk, risk_metrics.py:131-171).  risk_history
+    then still reports the distance-only combined risk of each state."""
     table = _table(duration, dt)
     steps = len(table) - 1
     starts = _starts(robots, start_index)
@@ -144,7 +150,7 @@ def run_hybrid_simulation(duration=20.0, dt=0.02, scenario="default", robots=1, 
     lp = nat.lqr_params(LQR_Q, LQR_R, dt, 2.0, 3.0)
     mp = nat.mpc_params(horizon, k["Q"], k["R"], k["P"], k["d_safe"], k["rho"], k["v_max"],
                         k["omega_max"], dt, block_size=block_size)
-    rp = nat.risk_params()
+    rp = nat.risk_params(use_predicted=use_predictive_risk)
     out = batch.rollout_batch("hybrid", steps, lparams=lp, mparams=mp, rparams=rp,
                               start_index=starts, x0=x0, obstacles=obs, table_len=len(table),
                               dt=dt, device=device)

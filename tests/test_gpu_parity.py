@@ -499,6 +499,29 @@ def test_rollout_hybrid_matches_oracle_closed_loop(rm):
 
 
 @pytest.mark.gpu
+def test_rollout_hybrid_predictive_risk_matches_oracle(rm):
+    """the switch fed with the last MPC solve's x_pred
+    (RmpcRiskParams.use_predicted; compute_predictive_risk, risk_metrics.py:131-171).  Not in
+    the reference's loop, so parity is against the oracle loop with the same option -- parity
+    unpinned by reference artefacts.  Weights chosen so that the predicted states change a
+    switching decision (checked on the oracle)."""
+    steps, s0 = 120, 0
+    rk = dict(alpha=0.3, beta=0.7, threshold_low=0.3)
+    rp = rm._native.risk_params(use_predicted=True, **rk)
+    lp = rm._native.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0)
+    mp = rm._native.mpc_params(6, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                               0.02, block_size=1)
+    out = rm.batch.rollout_batch("hybrid", steps, lparams=lp, mparams=mp, rparams=rp,
+                                 start_index=[s0], obstacles=ompc.default_obstacles())
+    st_o, ct_o, used_o = sims.hybrid_closed_loop(steps=steps, start=s0, predictive=True, risk_kwargs=rk)
+    _, _, used_plain = sims.hybrid_closed_loop(steps=steps, start=s0, risk_kwargs=rk)
+    assert (used_o != used_plain).any()
+    np.testing.assert_array_equal(out["used_mpc"][0], used_o)
+    np.testing.assert_allclose(out["controls"][0], ct_o, atol=1e-8, rtol=0)
+    np.testing.assert_allclose(out["states"][0], st_o, atol=1e-8, rtol=0)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["lqr", "mpc", "hybrid"])
 def test_rollout_shared_table_refs_equal_copied_segments(rm, monkeypatch, mode):
     """rollouts read each robot's reference segment straight from one
