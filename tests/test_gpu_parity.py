@@ -154,6 +154,40 @@ def test_mpc_kernel_matches_exact_qp_oracle(rm, N, bs, scen, ltv, noise, seed, B
         assert np.all(sc == 5)
 
 
+EXTRA8 = [(0.5, -0.5, 0.1), (-1.0, 0.0, 0.1), (0.3, 1.2, 0.12), (-1.2, -0.3, 0.1),
+          (1.8, 0.2, 0.1), (-1.8, -0.2, 0.1), (0.7, -1.1, 0.12), (-0.2, -0.1, 0.08)]
+
+
+@pytest.mark.parametrize("ltv,bs", [(True, 1), (True, 4), (False, 1)])
+def test_mpc_maximum_sizes_match_exact_qp_oracle(rm, ltv, bs):
+    """The ABI's limits: N = RMPC_MAX_HORIZON (64) with RMPC_MAX_OBSTACLES (16) obstacles
+    (the generic kernel: no lane-per-robot or lane-group instance at N = 64)."""
+    N, B = 64, 4
+    obs = ompc.union8_obstacles() + EXTRA8
+    assert len(obs) == 16
+    x0, xr, ur = _workload(N, B, 21, (0.2, 0.2, 0.3))
+    p = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                              0.02, block_size=bs, ltv=ltv)
+    out = rm.batch.mpc_solve_batch(p, x0, xr, ur, obs, step_count=np.full(B, 12, np.int32) if ltv else None)
+    assert np.all(out["status"] == 0)
+    oc = ompc.MPCController(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                            0.02, "OSQP", bs)
+    for b in range(B):
+        oc._step_count = 12
+        s = oc.solve_with_ltv(x0[b], xr[b], ur[b], obs) if ltv else oc.solve(x0[b], xr[b], ur[b], obs)
+        np.testing.assert_allclose(out["u_seq"][b], s.control_sequence, atol=1e-9, rtol=0)
+        np.testing.assert_allclose(out["x_pred"][b], s.predicted_states, atol=1e-9, rtol=0)
+        assert bool(out["slack_used"][b]) == s.slack_used
+    # one past each limit is an API error, not a silent truncation
+    with pytest.raises(rm.RmpcError):
+        p65 = rm._native.mpc_params(N + 1, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0,
+                                    3.0, 0.02, block_size=bs, ltv=ltv)
+        x0b, xrb, urb = _workload(N + 1, 1, 22)
+        rm.batch.mpc_solve_batch(p65, x0b, xrb, urb, obs)
+    with pytest.raises((ValueError, rm.RmpcError)):       # the wrapper checks before the C-ABI
+        rm.batch.mpc_solve_batch(p, x0[:1], xr[:1], ur[:1], obs + [(3.0, 3.0, 0.1)])
+
+
 @pytest.mark.parametrize("N,bs,scen,ltv,noise,seed,B", [CASES[1], CASES[2], CASES[4], CASES[5]])
 def test_mpc_generic_kernel_matches_exact_qp_oracle(rm, monkeypatch, N, bs, scen, ltv, noise, seed, B):
     """The generic lane-per-robot kernel alone (RMPC_DISABLE_FAST + RMPC_LTI_GENERIC): the
