@@ -778,58 +778,58 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         } else
 #endif
         {   // sequential sweep (block size > 1)
-        T x0 = d0, x1 = d1, x2 = d2;
-        // block record (bounds + gains) and step data of block j+1 loaded while j computes
-        T nx[16];
-        uint32_t nbf = 0;
-        auto ldf = [&](int j) __attribute__((always_inline)) {
+            T x0 = d0, x1 = d1, x2 = d2;
+            // block record (bounds + gains) and step data of block j+1 loaded while j computes
+            T nx[16];
+            uint32_t nbf = 0;
+            auto ldf = [&](int j) __attribute__((always_inline)) {
 #pragma unroll
-            for (int f = 0; f < 12; f++) nx[f] = base[RC::BLK + 12 * j + f];
+                for (int f = 0; f < 12; f++) nx[f] = base[RC::BLK + 12 * j + f];
 #pragma unroll
-            for (int f = 0; f < 4; f++) nx[12 + f] = BS == 1 ? base[RC::STEP + 12 * j + f] : (T)0;
-            nbf = BF(j);
-        };
-        ldf(0);
+                for (int f = 0; f < 4; f++) nx[12 + f] = BS == 1 ? base[RC::STEP + 12 * j + f] : (T)0;
+                nbf = BF(j);
+            };
+            ldf(0);
 #pragma unroll
-        for (int j = 0; j < NB; j++) {
-            T c[16];
+            for (int j = 0; j < NB; j++) {
+                T c[16];
 #pragma unroll
-            for (int f = 0; f < 16; f++) c[f] = nx[f];
-            const uint32_t bfj = nbf;
-            if (j + 1 < NB) ldf(j + 1);
-            __builtin_amdgcn_sched_barrier(0);
-            const T lo0 = c[0], hi0 = c[1], lo1 = c[2], hi1 = c[3];
-            const T e0 = c[4] * x0 + c[5] * x1 + c[6] * x2 + c[10];
-            const T e1 = c[7] * x0 + c[8] * x1 + c[9] * x2 + c[11];
-            const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
-            const T u0v = bf0 == 0 ? e0 : (bf0 == 1 ? lo0 : hi0);
-            const T u1v = bf1 == 0 ? e1 : (bf1 == 1 ? lo1 : hi1);
-            const int ns0 = box_rule_bf(bf0, e0, lo0, hi0, eps_b), ns1 = box_rule_bf(bf1, e1, lo1, hi1, eps_b);
-            bchg = bchg || ns0 != bf0 || ns1 != bf1;
-            NBF(j) = (uint32_t)(ns0 | (ns1 << 2));
-            GST(ZC(2 * j), u0v);
-            GST(ZC(2 * j + 1), u1v);
+                for (int f = 0; f < 16; f++) c[f] = nx[f];
+                const uint32_t bfj = nbf;
+                if (j + 1 < NB) ldf(j + 1);
+                __builtin_amdgcn_sched_barrier(0);
+                const T lo0 = c[0], hi0 = c[1], lo1 = c[2], hi1 = c[3];
+                const T e0 = c[4] * x0 + c[5] * x1 + c[6] * x2 + c[10];
+                const T e1 = c[7] * x0 + c[8] * x1 + c[9] * x2 + c[11];
+                const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
+                const T u0v = bf0 == 0 ? e0 : (bf0 == 1 ? lo0 : hi0);
+                const T u1v = bf1 == 0 ? e1 : (bf1 == 1 ? lo1 : hi1);
+                const int ns0 = box_rule_bf(bf0, e0, lo0, hi0, eps_b), ns1 = box_rule_bf(bf1, e1, lo1, hi1, eps_b);
+                bchg = bchg || ns0 != bf0 || ns1 != bf1;
+                NBF(j) = (uint32_t)(ns0 | (ns1 << 2));
+                GST(ZC(2 * j), u0v);
+                GST(ZC(2 * j + 1), u1v);
 #pragma unroll
-            for (int k = j * BS; k < (j + 1) * BS && k < N; k++) {
-                GST(XS(k, 0), x0); GST(XS(k, 1), x1); GST(XS(k, 2), x2);
-                const T sa0 = BS == 1 ? c[12] : STG(0, k), sa1 = BS == 1 ? c[13] : STG(1, k);
-                const T sb0 = BS == 1 ? c[14] : STG(2, k), sb1 = BS == 1 ? c[15] : STG(3, k);
-                const T n0 = x0 + sa0 * x2 + sb0 * u0v;
-                const T n1 = x1 + sa1 * x2 + sb1 * u0v;
-                const T n2 = x2 + dt * u1v;
-                x0 = n0; x1 = n1; x2 = n2;
+                for (int k = j * BS; k < (j + 1) * BS && k < N; k++) {
+                    GST(XS(k, 0), x0); GST(XS(k, 1), x1); GST(XS(k, 2), x2);
+                    const T sa0 = BS == 1 ? c[12] : STG(0, k), sa1 = BS == 1 ? c[13] : STG(1, k);
+                    const T sb0 = BS == 1 ? c[14] : STG(2, k), sb1 = BS == 1 ? c[15] : STG(3, k);
+                    const T n0 = x0 + sa0 * x2 + sb0 * u0v;
+                    const T n1 = x1 + sa1 * x2 + sb1 * u0v;
+                    const T n2 = x2 + dt * u1v;
+                    x0 = n0; x1 = n1; x2 = n2;
+                }
             }
-        }
-        GST(XS(N, 0), x0); GST(XS(N, 1), x1); GST(XS(N, 2), x2);
-        __syncthreads();
-        GPROF(4);
-        refresh();
-        // hinge rule per row (lane-parallel over steps)
-        for (int k = gl; k < N; k += G) {
-            const uint32_t h = HF(k), nh = hinge_rule(k, h, XS(k, 0), XS(k, 1));
-            NHF(k) = nh;
-            hchg = hchg || nh != h;
-        }
+            GST(XS(N, 0), x0); GST(XS(N, 1), x1); GST(XS(N, 2), x2);
+            __syncthreads();
+            GPROF(4);
+            refresh();
+            // hinge rule per row (lane-parallel over steps)
+            for (int k = gl; k < N; k += G) {
+                const uint32_t h = HF(k), nh = hinge_rule(k, h, XS(k, 0), XS(k, 1));
+                NHF(k) = nh;
+                hchg = hchg || nh != h;
+            }
         }
         const bool chg = gany<G>(bchg || hchg, grp);
         __syncthreads();
