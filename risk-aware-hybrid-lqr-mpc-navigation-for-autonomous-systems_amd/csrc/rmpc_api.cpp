@@ -340,9 +340,10 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         a.count = count;
         a.retry = (int32_t *)c->retry.p;
         a.retry_count = (int32_t *)c->retry_count.p;
-        // default cap (sweeps with the lane-group tail): 7 at N <= 20 (BASELINE config 3), 12
-        // beyond (config 4)
-        a.pdas_cap = getenv("RMPC_FAST_CAP") ? atoi(getenv("RMPC_FAST_CAP")) : (p->horizon <= 20 ? 7 : 12);
+        // default cap (sweeps with the lane-group tail): 7 at N <= 20 (BASELINE config 3; 9 for
+        // LTI, whose harder instances would otherwise overfill the tail), 12 beyond (config 4)
+        a.pdas_cap = getenv("RMPC_FAST_CAP") ? atoi(getenv("RMPC_FAST_CAP"))
+                                             : (p->horizon <= 20 ? (lti ? 9 : 7) : 12);
         const bool warm = !getenv("RMPC_COLD_TAIL");
         if (warm) {
             HIP_TRY(c->retry_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));

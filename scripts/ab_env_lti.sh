@@ -1,0 +1,11 @@
+#!/bin/bash
+# A/B of environment settings on the LTI (MPCController.solve) bench line.
+# Usage: bash scripts/ab_env_lti.sh "ENV=a ENV2=b" "ENV=c" ...   ("-" = defaults)
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+i=0
+for v in "$@"; do
+  i=$((i+1))
+  [ "$v" = "-" ] && v=""
+  env $v timeout -k 10 200 python bench.py --lti --steps 10 --warmup 2 --no-cpu-baseline --no-pcie > gpurun_out/ablti_$i.json 2>gpurun_out/ablti_$i.err || { echo "[$v] failed"; tail -5 gpurun_out/ablti_$i.err; exit 1; }
+  python -c "import json;d=json.load(open('gpurun_out/ablti_$i.json'));r=d.get('roofline',{});print('[$v] value %.4e ms/step %.4f'%(d['value'],d['ms_per_step']), r.get('stage_ms'), d.get('solver'))"
+done
