@@ -269,7 +269,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                       const double *obstacles, int32_t n_obs, int32_t *step_count, double *u0,
                       double *u_seq, double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
                       int32_t *iters, const int32_t *index, const int32_t *count, hipStream_t s,
-                      const int32_t *ref_off = nullptr) {
+                      const int32_t *ref_off = nullptr, int fast_cap = 0) {
     const int bs = p->formulation == RMPC_LTV ? p->block_size : 1;
     const MpcLayout L = rmpc_mpc_layout(p->horizon, bs, n_obs);
     HIP_TRY(ensure_ws(c, L, B));
@@ -342,8 +342,10 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         a.retry_count = (int32_t *)c->retry_count.p;
         // default cap (sweeps with the lane-group tail): 7 at N <= 20 (BASELINE config 3; 9 for
         // LTI, whose harder instances would otherwise overfill the tail), 12 beyond (config 4)
+        // (fast_cap: the caller's choice, e.g. the hybrid switch's MPC branch)
         a.pdas_cap = getenv("RMPC_FAST_CAP") ? atoi(getenv("RMPC_FAST_CAP"))
-                                             : (p->horizon <= 20 ? (lti ? 9 : 7) : 12);
+                     : fast_cap > 0           ? fast_cap
+                                              : (p->horizon <= 20 ? (lti ? 9 : 7) : 12);
         const bool warm = !getenv("RMPC_COLD_TAIL");
         if (warm) {
             HIP_TRY(c->retry_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
@@ -699,9 +701,12 @@ static int hybrid_step(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams
                                     u_out, nullptr, nullptr, nullptr, nullptr, (const int32_t *)c->idx_lqr.p,
                                     cnt, s));
     // MPC branch: solve_with_ltv on the segment; writes u0 straight into u_out
+    // the MPC branch holds only the robots near an obstacle: about half the batch, all of
+    // them in the hard part of the distribution, so the tail has room for more of them and a
+    // lower fast cap pays (BASELINE config 5 sweep: cap 6 77.9M against 76.4M at cap 7)
     return launch_mpc(c, mp, B, x, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs, step_count, u_out,
                       nullptr, pred, nullptr, (int32_t *)c->hyb_status.p, nullptr, nullptr,
-                      (const int32_t *)c->idx_mpc.p, cnt + 1, s, ref_off);
+                      (const int32_t *)c->idx_mpc.p, cnt + 1, s, ref_off, mp->horizon <= 20 ? 6 : 0);
 }
 
 extern "C" int rmpc_hybrid_step_batch_dev(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams *lp,
