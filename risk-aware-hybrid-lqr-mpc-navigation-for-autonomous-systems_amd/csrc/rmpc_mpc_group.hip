@@ -49,6 +49,7 @@ struct GroupArgs {
     int32_t *retry, *retry_count;     // not certified / non-finite -> generic kernel
     const uint32_t *warm;             // per list entry: hinge flags [N], box states [NB], iters
     int pdas_cap;                     // PDAS solves before projected Newton
+    double ls_beta;                   // Armijo backtracking factor (RMPC_LS_BETA, default 0.5)
     unsigned long long *prof;         // optional per-phase cycle counters (diagnostics)
     unsigned long long *prof_waves;   // optional per-wave phase records (RMPC_DENSE_PROF=2)
     int64_t nB;                       // rows of the per-robot output arrays (bounds checks)
@@ -1112,7 +1113,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
                         F = Ft;
                         searching = false;
                     }
-                    alpha *= (T)0.5;
+                    alpha *= (T)a.ls_beta;
                     continue;
                 }
 #endif
@@ -1135,7 +1136,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
                     F = Ft;
                     searching = false;
                 }
-                alpha *= (T)0.5;
+                alpha *= (T)a.ls_beta;
                 __syncthreads();
             }
             if (searching) fail = true;          // no acceptable step
@@ -1328,6 +1329,7 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
         a.chk = chk;
     }
     a.pdas_cap = pdas_cap < RMPC_PDAS_ITERS ? pdas_cap : RMPC_PDAS_ITERS;
+    a.ls_beta = getenv("RMPC_LS_BETA") ? atof(getenv("RMPC_LS_BETA")) : 0.5;
     const int G = group_lanes(N, bs), rpw = 64 / G;
     const size_t lds = (size_t)rpw * group_rec_bytes(N, bs, no, f32);
     const int64_t need = (capacity + rpw - 1) / rpw;
