@@ -19,6 +19,8 @@
 #include "rmpc_internal.h"
 #include "rmpc_riccati.h"
 
+#include <atomic>
+
 namespace rmpc {
 
 template <typename T>
@@ -678,12 +680,17 @@ static hipError_t launch_generic(const MpcDevParams &prm, const MpcLayout &L, in
     if (B <= 0) return hipSuccess;
     if (lds_lanes > 0) {
         const size_t lds = (size_t)L.REC * lds_lanes * sizeof(T);
-        static bool attr_set = false;
-        if (!attr_set) {
+        // the attribute is per device: one bit per device that has it (contexts on several
+        // GPUs may share a process)
+        static std::atomic<unsigned long long> attr_set{0};
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+        const unsigned long long bit = 1ull << (dev & 63);
+        if (!(attr_set.load() & bit)) {
             hipError_t e = hipFuncSetAttribute((const void *)mpc_solve_kernel<T, true>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (e != hipSuccess) return e;
-            attr_set = true;
+            attr_set.fetch_or(bit);
         }
         const int64_t blocks = (B + lds_lanes - 1) / lds_lanes;
         hipLaunchKernelGGL((mpc_solve_kernel<T, true>), dim3((unsigned)blocks), dim3(lds_lanes), lds,

@@ -1302,8 +1302,17 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
     a.warm = warm;
     a.prof = prof;
     a.prof_waves = nullptr;
-    static unsigned long long *pw = nullptr;
-    static int64_t pw_cap = 0;
+    // diagnostics buffers (RMPC_DENSE_PROF=2, RMPC_GROUP_CHECK): per thread and device
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    static thread_local int diag_dev = -1;
+    static thread_local unsigned long long *pw = nullptr;
+    static thread_local int64_t pw_cap = 0;
+    static thread_local int32_t *chk = nullptr;
+    if (diag_dev != dev) {                // buffers of another device are not reused here
+        pw = nullptr; pw_cap = 0; chk = nullptr;
+        diag_dev = dev;
+    }
     const int64_t waves_needed = (capacity + 64 / group_lanes(N, bs) - 1) / (64 / group_lanes(N, bs));
     if (prof && getenv("RMPC_DENSE_PROF") && atoi(getenv("RMPC_DENSE_PROF")) >= 2) {
         if (pw_cap < waves_needed) {
@@ -1318,8 +1327,7 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
     }
     a.nB = capacity;
     a.chk = nullptr;
-    static int32_t *chk = nullptr;                // RMPC_GROUP_CHECK=1: bounds-check flags
-    if (getenv("RMPC_GROUP_CHECK")) {
+    if (getenv("RMPC_GROUP_CHECK")) {             // RMPC_GROUP_CHECK=1: bounds-check flags
         if (!chk) {
             const hipError_t e = hipMalloc((void **)&chk, sizeof(int32_t));
             if (e != hipSuccess) return e;
