@@ -49,7 +49,7 @@ struct GroupArgs {
     int32_t *retry, *retry_count;     // not certified / non-finite -> generic kernel
     const uint32_t *warm;             // per list entry: hinge flags [N], box states [NB], iters
     int pdas_cap;                     // PDAS solves before projected Newton
-    double ls_beta;                   // Armijo backtracking factor (RMPC_LS_BETA, default 0.5)
+    double ls_beta;                   // Armijo backtracking: > 0 fixed factor, 0 quadratic interpolation
     unsigned long long *prof;         // optional per-phase cycle counters (diagnostics)
     unsigned long long *prof_waves;   // optional per-wave phase records (RMPC_DENSE_PROF=2)
     int64_t nB;                       // rows of the per-robot output arrays (bounds checks)
@@ -515,7 +515,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
     // One Armijo trial of the projected-Newton search (BS = 1), fused: each lane forms its
     // steps' trial inputs z_t = clamp(z + alpha (z_c - z)) and their gradient term, rolls
     // out and costs them, and -- when the group accepts -- writes them to ZZ itself.
-    auto ls_trial = [&](T alpha, bool m, T Fc, bool &acc) __attribute__((always_inline)) -> T {
+    auto ls_trial = [&](T alpha, bool m, T Fc, bool &acc, T &gdo) __attribute__((always_inline)) -> T {
         refresh();
         const int k0 = gl * CH;
         T w0[CH], w1[CH], gd = 0;
@@ -533,6 +533,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         int u;
         const T Ft = rollout_cost(w0, w1, m, u);
         gd = gsum<G>(gd);
+        gdo = gd;
         acc = m && Ft <= Fc + (T)1e-4 * gd;
         if (acc) {
 #pragma unroll
@@ -1108,12 +1109,19 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
 #if RMPC_GROUP_SCAN
                 if constexpr (BS == 1) {
                     bool acc;
-                    const T Ft = ls_trial(alpha, searching, F, acc);
+                    T gd;
+                    const T Ft = ls_trial(alpha, searching, F, acc, gd);
                     if (acc) {
                         F = Ft;
                         searching = false;
                     }
-                    alpha *= (T)a.ls_beta;
+                    if (a.ls_beta > 0) {
+                        alpha *= (T)a.ls_beta;
+                    } else {       // safeguarded quadratic interpolation: q(s) = F + gd s + c s^2, q(1) = Ft
+                        const T c = Ft - F - gd;
+                        const T s = c > (T)0 ? -gd / ((T)2 * c) : (T)0.5;
+                        alpha *= fmin(fmax(s, (T)0.1), (T)0.5);
+                    }
                     continue;
                 }
 #endif
@@ -1136,7 +1144,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
                     F = Ft;
                     searching = false;
                 }
-                alpha *= (T)a.ls_beta;
+                alpha *= (T)(a.ls_beta > 0 ? a.ls_beta : 0.5);   // (block size > 1: fixed factor)
                 __syncthreads();
             }
             if (searching) fail = true;          // no acceptable step
@@ -1337,7 +1345,8 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
         a.chk = chk;
     }
     a.pdas_cap = pdas_cap < RMPC_PDAS_ITERS ? pdas_cap : RMPC_PDAS_ITERS;
-    a.ls_beta = getenv("RMPC_LS_BETA") ? atof(getenv("RMPC_LS_BETA")) : 0.5;
+    // Armijo backtracking: safeguarded quadratic interpolation (0, default), or a fixed factor
+    a.ls_beta = getenv("RMPC_LS_BETA") ? atof(getenv("RMPC_LS_BETA")) : 0.0;
     const int G = group_lanes(N, bs), rpw = 64 / G;
     const size_t lds = (size_t)rpw * group_rec_bytes(N, bs, no, f32);
     const int64_t need = (capacity + rpw - 1) / rpw;
