@@ -93,7 +93,8 @@ def main():
     ap.add_argument("--config", default="cfg3", choices=["cfg2", "cfg3", "cfg4", "cfg5"],
                     help="BASELINE config (cfg3 = the metric's configuration, the default)")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-pointer (PCIe-inclusive) timing")
-    ap.add_argument("--f32", action="store_true", help="fp32 arithmetic for cfg3 too (A/B; cfg4 is fp32 always)")
+    ap.add_argument("--f32", action="store_true", help="fp32 arithmetic for cfg3 too (A/B)")
+    ap.add_argument("--f64", action="store_true", help="fp64 arithmetic for cfg4 (A/B against its fp32 pipeline)")
     ap.add_argument("--lti", action="store_true",
                     help="MPCController.solve (absolute-state LTI, mpc_node's path) instead of solve_with_ltv")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -134,16 +135,21 @@ def main():
     B = idx.size
 
     # ---- synthetic inputs (Figure-8 offsets + seeded noise), generated by the device
-    # reference kernel and then made resident in HBM before anything is timed
-    t0 = W.t0_at(idx, B_total)
-    xr_h, ur_h = rmpc.batch.figure8_batch(t0, N + 1, device=local)
-    x0_h = xr_h[:, 0] + W.noise_at(idx, seed)
-    dev = torch.device(f"cuda:{local}")
-    x0 = torch.from_numpy(x0_h).to(dev)
-    xr = torch.from_numpy(xr_h).to(dev)
-    ur = torch.from_numpy(ur_h).to(dev)
-    obs = torch.tensor(obs_list, dtype=torch.float64, device=dev).reshape(-1, 3)
+    # reference kernel and then made resident in HBM before anything is timed.  Each batch in
+    # flight is its own fleet (rmpc.workloads.fleet_t0 / fleet_seed: other reference offsets,
+    # other start noise): one fleet's closed loop cannot overlap its own steps, so the batches
+    # in flight stand for independent fleets sharing the GPU, not copies of one batch.
     S = max(1, args.inflight)
+    dev = torch.device(f"cuda:{local}")
+    fleets = []
+    for f in range(S):
+        xr_f, ur_f = rmpc.batch.figure8_batch(W.fleet_t0(idx, B_total, f, S), N + 1, device=local)
+        x0_f = xr_f[:, 0] + W.noise_at(idx, W.fleet_seed(seed, f))
+        fleets.append(dict(x0_h=x0_f, xr_h=xr_f, ur_h=ur_f, x0=torch.from_numpy(x0_f).to(dev),
+                           xr=torch.from_numpy(xr_f).to(dev), ur=torch.from_numpy(ur_f).to(dev)))
+    x0_h, xr_h, ur_h = fleets[0]["x0_h"], fleets[0]["xr_h"], fleets[0]["ur_h"]
+    x0, xr, ur = fleets[0]["x0"], fleets[0]["xr"], fleets[0]["ur"]
+    obs = torch.tensor(obs_list, dtype=torch.float64, device=dev).reshape(-1, 3)
 
     def new_out():
         return dict(u0=torch.empty(B, 2, dtype=torch.float64, device=dev),
@@ -159,7 +165,7 @@ def main():
     counts_sc = [torch.full((B,), 10, dtype=torch.int32, device=dev) for _ in range(S)]   # past the cold-start ramp
     step_count = counts_sc[0]
     # config 4 is specified in fp32 arithmetic (BASELINE.json); config 3 in fp64
-    f32 = args.config == "cfg4" or args.f32
+    f32 = (args.config == "cfg4" and not args.f64) or args.f32
     p = rmpc._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
                                 0.02, block_size=1, ltv=not args.lti, precision=1 if f32 else 0)
     stream = torch.cuda.current_stream()
@@ -170,7 +176,7 @@ def main():
     # against (9, 4), config 4 (14, 6) against (12, 6)
     caps = (0, 0)
     if S > 1:
-        caps = (14, 6) if f32 else ((13, 4) if args.lti else (9, 4))
+        caps = (14, 6) if N > 20 else ((13, 4) if args.lti else (9, 4))
     if args.stage_caps:
         caps = tuple(int(v) for v in args.stage_caps.split(","))
     for i in range(S):
@@ -178,9 +184,13 @@ def main():
 
     def step(k=0):
         i = k % S
-        rmpc.batch.mpc_solve_batch_dev(p, x0, xr, ur, obs, outs[i], step_count=counts_sc[i],
+        fl = fleets[i]
+        rmpc.batch.mpc_solve_batch_dev(p, fl["x0"], fl["xr"], fl["ur"], obs, outs[i], step_count=counts_sc[i],
                                        device=local, stream=streams[i], slot=i)
 
+    # inputs, outputs and step counters were written on the default stream: the other
+    # streams start only after that work (they are non-blocking streams)
+    torch.cuda.synchronize()
     for k in range(max(args.warmup, S)):
         step(k)
     torch.cuda.synchronize()
@@ -243,18 +253,17 @@ def main():
 
         def step_gather():
             step()
-            dist.all_gather_into_tensor(g_out, out["u0"])
+            return W.gather_interleaved(dist, out["u0"], world, g_out)[0]
         step_gather()
         torch.cuda.synchronize()
         dist.barrier()
         torch.cuda.synchronize()
         t_g = time.perf_counter()
         for _ in range(args.steps):
-            step_gather()
+            u0_global = step_gather()
         torch.cuda.synchronize()
         dist.barrier()
         elapsed_g = time.perf_counter() - t_g
-        u0_global = g_out.view(world, B, 2).transpose(0, 1).reshape(-1, 2)
         assert torch.equal(u0_global[rank::world], out["u0"])
         tt = torch.tensor([elapsed_g], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -385,10 +394,24 @@ def main():
         cpu.mpc_solve_batch(cp, x0_h[s1], xr_h[s1], ur_h[s1], obs_list,
                             step_count=np.full(n1, 10, np.int32), threads=1)
         t1 = time.perf_counter() - t
-        cpu.set_pdas_caps(0, 0)
         gpu_useq = out["u_seq"].cpu().numpy()[sl]
         both = (res["status"] == 0) & (st[sl] == 0)
         du = float(np.abs(gpu_useq[both] - res["u_seq"][both]).max())
+        # every fleet in flight against the port on a strided 4096-robot sample of its own
+        # inputs (the last timed step of its slot): u_seq and x_pred
+        du_fleet = []
+        for f in range(S):
+            fl, of = fleets[f], outs[f]
+            s4 = slice(0, B, max(1, B // 4096))
+            rf = cpu.mpc_solve_batch(cp, fl["x0_h"][s4], fl["xr_h"][s4], fl["ur_h"][s4], obs_list,
+                                     step_count=np.full(len(range(*s4.indices(B))), 10, np.int32),
+                                     threads=threads)
+            ok = (rf["status"] == 0) & (of["status"].cpu().numpy()[s4] == 0)
+            du_fleet.append({
+                "u_seq": float(np.abs(of["u_seq"].cpu().numpy()[s4][ok] - rf["u_seq"][ok]).max()),
+                "x_pred": float(np.abs(of["x_pred"].cpu().numpy()[s4][ok] - rf["x_pred"][ok]).max()),
+                "optimal_both": int(ok.sum())})
+        cpu.set_pdas_caps(0, 0)
         line["cpu_baseline"] = {
             "value": nsamp * reps / t_cpu, "unit": "solves/s", "cores": threads, "kind": "port",
             "sample": f"{nsamp} robots (every {B // nsamp}th) of the same workload x {reps} reps "
@@ -400,6 +423,7 @@ def main():
         if f32:
             line["cpu_baseline"]["note"] = "the C port computes in fp64 (the GPU path in fp32)"
         line["max_abs_du_vs_cpu_port"] = du
+        line["max_abs_diff_vs_cpu_port_per_fleet"] = du_fleet
     # HBM traffic per launch from the committed PMC passes of this workload (rocprofv3 --pmc
     # FETCH_SIZE / WRITE_SIZE in separate runs, gfx950 corrections: scripts/pmc_traffic.py)
     if args.config == "cfg3" and not args.lti and not f32:
@@ -431,6 +455,7 @@ def _timed(args, step, dist, dev, S=1):
     own device time).  Returns (elapsed s, event ms list)."""
     import torch
     stream = torch.cuda.current_stream()
+    torch.cuda.synchronize()       # per-slot state written on the default stream comes first
     for k in range(max(args.warmup, S)):
         step(k)
     torch.cuda.synchronize()
@@ -522,17 +547,20 @@ def bench_other(args, world, rank, local, dist, pre=None):
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(S - 1)]
     lp = rmpc._native.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0, use_cache=False)
     if args.config == "cfg2":
-        t0 = W.t0_at(idx, B_total)
-        xr_h, ur_h = rmpc.batch.figure8_batch(t0, 1, device=local)
-        x_h = xr_h[:, 0] + W.noise_at(idx, cfg["seed"])
-        x = torch.from_numpy(x_h).to(dev)
-        xr = torch.from_numpy(np.ascontiguousarray(xr_h[:, 0])).to(dev)
-        ur = torch.from_numpy(np.ascontiguousarray(ur_h[:, 0])).to(dev)
+        fleets = []                      # one fleet per slot in flight (rmpc.workloads.fleet_t0)
+        for f in range(S):
+            xr_f, ur_f = rmpc.batch.figure8_batch(W.fleet_t0(idx, B_total, f, S), 1, device=local)
+            x_f = xr_f[:, 0] + W.noise_at(idx, W.fleet_seed(cfg["seed"], f))
+            fleets.append((x_f, xr_f, ur_f))
+        x_h, xr_h, ur_h = fleets[0]
+        dfl = [(torch.from_numpy(a).to(dev), torch.from_numpy(np.ascontiguousarray(b[:, 0])).to(dev),
+                torch.from_numpy(np.ascontiguousarray(c[:, 0])).to(dev)) for a, b, c in fleets]
         us = [torch.empty(B, 2, dtype=torch.float64, device=dev) for _ in range(S)]
         sts = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(S)]
 
         def step(k=0):
             i = k % S
+            x, xr, ur = dfl[i]
             rmpc.batch.lqr_control_batch_dev(lp, x, xr, ur, us[i], status=sts[i], device=local,
                                              stream=streams[i], slot=i)
         metric, unit = "LQR control steps/sec (DARE + gain + control per robot, no cache)", "controls/s"
@@ -541,13 +569,16 @@ def bench_other(args, world, rank, local, dist, pre=None):
     else:
         # ~half the robots within 0.767 m of an obstacle edge (MPC branch), half farther
         # (rmpc.workloads.cfg5_t0; tests/test_gpu_fullsize.py checks this exact workload)
-        t0 = W.cfg5_t0(idx)
         N = cfg["N"]
-        xr_h, ur_h = rmpc.batch.figure8_batch(t0, N + 1, device=local)
-        x_h = xr_h[:, 0] + W.noise_at(idx, cfg["seed"])
-        x = torch.from_numpy(x_h).to(dev)
-        xr = torch.from_numpy(xr_h).to(dev)
-        ur = torch.from_numpy(ur_h).to(dev)
+        # one fleet per slot in flight: fleet f's robots are the config's with other start
+        # noise (the arc pools of cfg5_t0 fix which robots are near an obstacle)
+        fleets = []
+        for f in range(S):
+            xr_f, ur_f = rmpc.batch.figure8_batch(W.cfg5_t0(idx), N + 1, device=local)
+            x_f = xr_f[:, 0] + W.noise_at(idx, W.fleet_seed(cfg["seed"], f))
+            fleets.append((torch.from_numpy(x_f).to(dev), torch.from_numpy(xr_f).to(dev),
+                           torch.from_numpy(ur_f).to(dev), x_f))
+        x_h, xr_h, ur_h = fleets[0][3], fleets[0][1].cpu().numpy(), fleets[0][2].cpu().numpy()
         obs = torch.tensor(W.DEFAULT_OBS, dtype=torch.float64, device=dev)
         mp = rmpc._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
                                      0.02, block_size=1)
@@ -562,7 +593,11 @@ def bench_other(args, world, rank, local, dist, pre=None):
         useds = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(S)]
         risks = [torch.empty(B, dtype=torch.float64, device=dev) for _ in range(S)]
         used = useds[0]
-        lp = rmpc._native.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0)
+        # The LQR branch without the gain cache (`lp` above, use_cache=False): in the reference
+        # loop the reference index advances every step (run_simulation.py:525-526), so the
+        # operating point moves and compute_gain's 1e-6 cache (lqr_controller.py:112-114) misses:
+        # every LQR-branch robot solves its DARE every step.  Here the inputs repeat from step
+        # to step, and a cache would turn every step after the first into a cached clip.
 
         # in flight, the MPC branch's first stage runs longer (scripts/r02_s3_caps_cfg.sh:
         # fast cap 9 against the single-batch default 6)
@@ -572,6 +607,7 @@ def bench_other(args, world, rank, local, dist, pre=None):
 
         def step(k=0):
             i = k % S
+            x, xr, ur, _ = fleets[i]
             rmpc.batch.hybrid_step_batch_dev(rp, lp, mp, x, xr, ur, obs, states[i], us[i], useds[i], risks[i],
                                              device=local, stream=streams[i], slot=i)
         metric, unit = "hybrid LQR/MPC control steps/sec (risk + dwell switch + branch)", "steps/s"
@@ -651,7 +687,7 @@ def bench_other(args, world, rank, local, dist, pre=None):
             sl = slice(0, B, B // nsamp)
             xs, xrs, urs = x_h[sl], xr_h[sl], ur_h[sl]
             cp = cpu.mpc_params(N, (15, 15, 50), (.1, .1), (30, 30, 40), 0.3, 5000., 2., 3., 0.02)
-            lq = cpu.lqr_params((15, 15, 8), (.1, .1), 0.02, 2.0, 3.0)
+            lq = cpu.lqr_params((15, 15, 8), (.1, .1), 0.02, 2.0, 3.0, use_cache=0)   # as the GPU leg
 
             def cpu_step():
                 d = np.min([np.hypot(xs[:, 0] - ox, xs[:, 1] - oy) - r for ox, oy, r in W.DEFAULT_OBS], 0)

@@ -18,6 +18,18 @@ from .qp import solve_qp
 KP_FALLBACK = np.array([[1.0, 0.0, 0.0], [0.0, 0.0, 0.5]])   # mpc_controller.py:327-328
 
 
+class OracleFailure(RuntimeError):
+    """The exact QP oracle did not converge ("max_iter"): a failure of the checker, never a
+    verdict on the QP -- so it is raised, not turned into the reference's fallback law (which
+    the reference applies only when CVXPY reports the problem infeasible/unsolved,
+    mpc_controller.py:521-522)."""
+
+
+def _check_converged(res):
+    if res.status == "max_iter":
+        raise OracleFailure(f"oracle/qp.py: no convergence in {res.iters} iterations")
+
+
 class Solution:
     def __init__(self, status, u0, u_seq, x_pred, cost, slack_used, iters=0, qp_status=""):
         self.status = status
@@ -169,6 +181,7 @@ class MPCController:
         H, c, const, E, f, G, h, L = self.build_ltv(x0, x_refs, u_refs, obstacles,
                                                     use_soft_constraints)
         res = solve_qp(H, c, E, f, G, h)
+        _check_converged(res)
         if res.status != "optimal":
             return self.fallback(x0, x_refs, u_refs)                        # :521-522
         w = res.w
@@ -284,6 +297,7 @@ class MPCController:
         H, c, const, E, f, G, h, L = self.build_lti(x0, x_refs, u_refs, obstacles,
                                                     use_soft_constraints)
         res = solve_qp(H, c, E, f, G, h)
+        _check_converged(res)
         if res.status != "optimal":
             return self.fallback(x0, L["x_refs"], L["u_refs"])
         w = res.w

@@ -79,6 +79,7 @@ struct RmpcCtx {
     DevBuf idx_lqr, idx_mpc, counts, hyb_status;
     DevBuf fast_gains, retry, retry2, retry_count, prof, retry_sets;
     DevBuf retry_a, retry_sets_a;   // two-pass fast stage: the first pass's list and sets
+    DevBuf refine, refine_sets;     // fp32 requests: the fp32-certified robots and their sets
     GroupDiag gdiag;           // lane-group tail diagnostics (RMPC_GROUP_CHECK, RMPC_DENSE_PROF=2)
     // closed-loop rollout state (rmpc_rollout_batch)
     DevBuf ro_x, ro_xr, ro_ur, ro_u, ro_step, ro_cache, ro_prev, ro_since, ro_status, ro_used,
@@ -243,6 +244,8 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     c->retry_sets.release();
     c->retry_a.release();
     c->retry_sets_a.release();
+    c->refine.release();
+    c->refine_sets.release();
     for (DevBuf *d : {&c->ro_x, &c->ro_xr, &c->ro_ur, &c->ro_u, &c->ro_step, &c->ro_cache, &c->ro_prev,
                       &c->ro_since, &c->ro_status, &c->ro_used, &c->ro_risk, &c->ro_counts, &c->ro_off, &c->ro_pred})
         d->release();
@@ -431,7 +434,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
     const bool f32 = p->precision == RMPC_F32;
     // hard half-spaces (soft = 0 with obstacles): augmented-Lagrangian rounds in the generic kernel
     const bool hard = !p->soft && n_obs > 0;
-    const bool fast = !hard && rmpc_mpc_fast_supported(p->horizon, bs, p->precision, p->formulation == RMPC_LTI) &&
+    const bool fast = !hard && rmpc_mpc_fast_supported(p->horizon, bs, p->precision, p->formulation == RMPC_LTI, n_obs) &&
                       !rmpc_knob("RMPC_DISABLE_FAST");
     // fp64 without a lane-per-robot instance -- LTI (MPCController.solve, mpc_node's path),
     // or an LTV (N, block size) the fast kernel is not built for (N = 30) -- every robot
@@ -526,6 +529,22 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         // (RMPC_FAST_SPLIT=<first-pass cap>, A/B only; default 0 = one pass: measured slower)
         const int split = rmpc_knob("RMPC_FAST_SPLIT") ? atoi(rmpc_knob("RMPC_FAST_SPLIT")) : 0;
         const bool two_pass = warm && split > 0 && split < a.pdas_cap && B >= 8192;
+        // Mixed precision for fp32 requests (BASELINE config 4): the fp32 lane-per-robot pass
+        // only finds the active sets.  Every robot it certifies goes on, with its sets, to an
+        // fp64 pass of the same kernel that re-solves the equality-constrained QP of those sets
+        // in fp64, re-checks them (KKT) and continues PDAS from them if they change (up to
+        // `extra_cap` solves); it writes the outputs, which are therefore fp64-exact.  What it
+        // does not certify joins the fp64 tail's list.  (RMPC_NO_REFINE=1: the fp32 pass writes
+        // its own outputs, the round-2 behaviour; A/B only)
+        const bool refine = f32 && warm && !two_pass && rmpc_mpc_refine_supported(p->horizon, bs, n_obs) &&
+                            !rmpc_knob("RMPC_NO_REFINE");
+        if (refine) {
+            HIP_TRY(c->refine.ensure((size_t)B * sizeof(int32_t)));
+            HIP_TRY(c->refine_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
+            a.refine = (int32_t *)c->refine.p;
+            a.refine_count = cnt + 6;
+            a.refine_sets = (uint32_t *)c->refine_sets.p;
+        }
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[0], s));
         if (two_pass) {
             HIP_TRY(c->retry_a.ensure((size_t)B * sizeof(int32_t)));
@@ -542,6 +561,16 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             a.warm_sets = a1.retry_sets;
         }
         HIP_TRY(rmpc_launch_mpc_fast(a, p->horizon, bs, p->precision, s, lti));
+        if (refine) {
+            dbg_sync(s, "fast (fp32 sets)");
+            MpcFastArgs r = a;
+            r.refine = nullptr; r.refine_count = nullptr; r.refine_sets = nullptr;
+            r.index = a.refine;
+            r.count = a.refine_count;
+            r.warm_sets = a.refine_sets;
+            r.extra_cap = rmpc_knob("RMPC_REFINE_CAP") ? atoi(rmpc_knob("RMPC_REFINE_CAP")) : 4;
+            HIP_TRY(rmpc_launch_mpc_fast(r, p->horizon, bs, RMPC_F64, s, lti));
+        }
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[1], s));
         dbg_sync(s, "fast");
         const int32_t *left = (const int32_t *)c->retry.p;

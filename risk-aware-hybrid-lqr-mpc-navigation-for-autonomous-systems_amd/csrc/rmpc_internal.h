@@ -68,11 +68,20 @@ struct MpcFastArgs {
                                      // start of the next stage (may be null)
     const uint32_t *warm_sets;       // continuing pass: the previous pass's retry_sets, read by
                                      // list position (null: cold start from empty sets)
+    int extra_cap;                   // > 0 (with warm_sets): PDAS solves beyond the record's count
+                                     // (the fp64 refinement pass) instead of pdas_cap in total
+    // fp32 pass of a refined request (non-null): certified robots are appended here with their
+    // sets (same record layout as retry_sets) for the fp64 refinement pass, which writes their
+    // outputs; uncertified ones still go to `retry`
+    int32_t *refine, *refine_count;
+    uint32_t *refine_sets;
 };
 // list counters per set of a context (retry_count holds two sets, used by alternate calls)
 #define RMPC_COUNT_WORDS 16
 
-bool rmpc_mpc_fast_supported(int N, int bs, int prec, bool lti = false);
+bool rmpc_mpc_fast_supported(int N, int bs, int prec, bool lti = false, int no = -1);
+// an fp64 lane-per-robot instance that continues an fp32 request's certified sets
+bool rmpc_mpc_refine_supported(int N, int bs, int no);
 bool rmpc_mpc_dense_supported(int N, int bs, int no);
 hipError_t rmpc_launch_mpc_dense_f64(const MpcDevParams &prm, int N, int bs, int no, int64_t capacity,
                                      const double *x0, const double *x_refs, int ref_rows,

@@ -63,9 +63,27 @@ struct WaveRows {
 template <typename T> struct GainTile;
 template <> struct GainTile<double> {
     WaveRows<16> w;
-    __device__ __forceinline__ GainTile(void *base, int nb, int lane) : w(base, nb * 4, lane) {}
-    __device__ __forceinline__ void st_half(int, const double *, int) const {}   // (paired lanes: fp32 only)
-    __device__ __forceinline__ void ld_pair(int, double *, int) const {}
+    __device__ __forceinline__ GainTile(void *base, int nb, int lane, int pr = 1) : w(base, nb * 4 / pr, lane) {}
+    // Paired lanes (the fp64 refinement of config 4): two rows per block; in row 2j+q lane 2r's
+    // slot holds G[2q], G[2q+1] and lane 2r+1's slot G[4+2q], G[5+2q].  Each lane stores its
+    // half and reads both halves back (the pair's gains are bitwise identical).
+    __device__ __forceinline__ void st_half(int j, const double G[8], int pp) const {
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+            w.st16(2 * j + q, __builtin_bit_cast(u4v, make_double2(G[4 * pp + 2 * q], G[4 * pp + 2 * q + 1])));
+    }
+    __device__ __forceinline__ void ld_pair(int j, double G[8], int pp) const {
+        const unsigned v0 = w.vo - (unsigned)pp * 16u;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const double2 x = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(
+                w.r, v0, (2 * j + q) * RMPC_WAVE * 16, RMPC_GAIN_LD_AUX));
+            const double2 y = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(
+                w.r, v0 + 16u, (2 * j + q) * RMPC_WAVE * 16, RMPC_GAIN_LD_AUX));
+            G[2 * q] = x.x; G[2 * q + 1] = x.y;
+            G[4 + 2 * q] = y.x; G[5 + 2 * q] = y.y;
+        }
+    }
     __device__ __forceinline__ void st(int j, const double G[8]) const {
 #pragma unroll
         for (int q = 0; q < 4; q++) w.st16(j * 4 + q, __builtin_bit_cast(u4v, make_double2(G[2 * q], G[2 * q + 1])));
@@ -81,7 +99,7 @@ template <> struct GainTile<double> {
 };
 template <> struct GainTile<float> {
     WaveRows<16> w;
-    __device__ __forceinline__ GainTile(void *base, int nb, int lane) : w(base, nb * 2, lane) {}
+    __device__ __forceinline__ GainTile(void *base, int nb, int lane, int = 1) : w(base, nb * 2, lane) {}
     // Paired lanes (two lanes per robot, identical gains): each lane stores one half of the
     // block's 8 values (lane 2r: G0..3 in row 2j, lane 2r+1: G4..7 in row 2j+1, both at the
     // pair's own lane offsets) and reads both halves back.
@@ -237,7 +255,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     const double *ur = a.u_refs + ref_row0(a.prm.ref_off, b, a.uref_rows) * 2;
     // per-wave gain tile (sized for fp64; fp32 uses half)
     // (paired lanes, fp32: twice the waves, each with an fp32-sized tile -- the same buffer)
-    const GainTile<T> gt(a.gains + (size_t)blockIdx.x * NB * (PR == 2 ? 2 : 4) * RMPC_WAVE, NB, lane);
+    const GainTile<T> gt(a.gains + (size_t)blockIdx.x * NB * (PR == 2 ? 2 : 4) * RMPC_WAVE, NB, lane, PR);
 
     // ---- setup: np.unwrap'd reference heading, linearisation data (mpc_controller.py:391-428)
     // sin/cos of the heading and the reference speed stay in VGPRs; the reference position
@@ -245,10 +263,14 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     // The unwrap and sin/cos run in fp64 for both T.
     extern __shared__ double lds_raw[];
     T *const lds = reinterpret_cast<T *>(lds_raw);
+    // [field][k][robot of the wave]: paired lanes share their robot's entries (both lanes write
+    // the same value; both read it -- a broadcast), so a paired wave holds 32 columns
+    constexpr int LW = RMPC_WAVE / PR;
+    const int ll = lane / PR;
     T S[N], Cs[N], V0[N];
-#define PX(k) lds[(0 * N + (k)) * RMPC_WAVE + lane]
-#define PY(k) lds[(1 * N + (k)) * RMPC_WAVE + lane]
-#define V1(k) lds[(2 * N + (k)) * RMPC_WAVE + lane]
+#define PX(k) lds[(0 * N + (k)) * LW + ll]
+#define PY(k) lds[(1 * N + (k)) * LW + ll]
+#define V1(k) lds[(2 * N + (k)) * LW + ll]
     bool fin = true;
     T d0, d1, d2;
     T la0 = 0, la1 = 0, lb0 = 0, lb1 = 0;        // LTI: the one linearisation
@@ -291,7 +313,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         const bool coal = F64 && PR == 1 && (int64_t)(blockIdx.x + 1) * RMPC_WAVE <= n;
         if (coal) {
             constexpr int SP = 17;                           // scratch row stride in doubles (bank spread)
-            double *const stg = lds_raw + (size_t)3 * N * RMPC_WAVE * sizeof(T) / sizeof(double);
+            double *const stg = lds_raw + (size_t)3 * N * LW * sizeof(T) / sizeof(double);
             const int64_t t0 = (int64_t)blockIdx.x * RMPC_WAVE;
             const int rr = lane >> 4, ee = lane & 15;
             // all of an array's loads are issued before the first LDS round (one memory latency
@@ -372,7 +394,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
 
     int it = 0, cert = 0, used = 0;
     T J = 0;
-    const int maxit = min(p.max_iter, a.pdas_cap);
+    const int maxit0 = min(p.max_iter, a.pdas_cap);
     unsigned long long tp_b = 0, tp_f = 0, tp0 = a.prof ? __builtin_amdgcn_s_memtime() : 0ull;
     const unsigned long long tp_setup = tp0;
     uint64_t hist0 = 0, hist1 = 0, hist2 = 0, hist3 = 0;   // active-set signatures (cycles)
@@ -409,6 +431,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         it = (int)ws[(N + NB) * a.B];
         if (it > 0) hist0 = set_sig();
     }
+    // (fp64 refinement of fp32-certified sets: `extra_cap` more PDAS solves from them)
+    const int maxit = a.extra_cap > 0 ? min(p.max_iter, it + a.extra_cap) : maxit0;
     while (fin && it < maxit) {
         it++;
         // Keep the per-step inputs opaque to the optimiser at every iteration: otherwise it
@@ -459,10 +483,10 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                     pxk = pxb; pyk = pyb; v1k = v1b;
                     if (k > 0) {
                         if (RMPC_BPF == 1) {    // (2: positions loaded in the rows' branch)
-                            pxb = lds[(0 * N + k - 1) * RMPC_WAVE + lane + anc];
-                            pyb = lds[(1 * N + k - 1) * RMPC_WAVE + lane + anc];
+                            pxb = lds[(0 * N + k - 1) * LW + ll + anc];
+                            pyb = lds[(1 * N + k - 1) * LW + ll + anc];
                         }
-                        v1b = lds[(2 * N + k - 1) * RMPC_WAVE + lane + anc];
+                        v1b = lds[(2 * N + k - 1) * LW + ll + anc];
                     }
                 } else {
                     v1k = V1(k);
@@ -643,7 +667,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                                  "+v"(used), "+v"(Hf.w[k >> 1]), "+v"(Bf.w[j >> 3]));
                 const T v1k = FPF ? v1n : V1(k);     // reference turn rate (LTV; LTI: heading, unused here)
                 if constexpr (FPF) {
-                    if (k + 1 < N) v1n = lds[(2 * N + k + 1) * RMPC_WAVE + lane + anc];
+                    if (k + 1 < N) v1n = lds[(2 * N + k + 1) * LW + ll + anc];
                 }
                 T lo0, hi0, lo1, hi1;
                 if constexpr (LTI) {
@@ -676,12 +700,12 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                 if constexpr (FPF) {
                     px = pxn; py = pyn;
                     if (k + 1 < N) {
-                        pxn = lds[(0 * N + k + 1) * RMPC_WAVE + lane + anc];
-                        pyn = lds[(1 * N + k + 1) * RMPC_WAVE + lane + anc];
+                        pxn = lds[(0 * N + k + 1) * LW + ll + anc];
+                        pyn = lds[(1 * N + k + 1) * LW + ll + anc];
                     }
                 } else {
-                    px = lds[(0 * N + k) * RMPC_WAVE + lane + anc];
-                    py = lds[(1 * N + k) * RMPC_WAVE + lane + anc];
+                    px = lds[(0 * N + k) * LW + ll + anc];
+                    py = lds[(1 * N + k) * LW + ll + anc];
                 }
                 const T *const ob = obs_s + anc;
                 bool usd = false;
@@ -773,7 +797,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                 const T uu0 = LTI ? u0v : u0v + V0[k], uu1 = LTI ? u1v : u1v + V1(k);
                 J += R0 * uu0 * uu0 + R1 * uu1 * uu1;
                 uint32_t hk = Hf.get(k);
-                const T px = lds[(0 * N + k) * RMPC_WAVE + lane + anc], py = lds[(1 * N + k) * RMPC_WAVE + lane + anc];
+                const T px = lds[(0 * N + k) * LW + ll + anc], py = lds[(1 * N + k) * LW + ll + anc];
                 const T *const ob = obs_s + anc;
                 T cx = ob[0], cy = ob[1], cs = ob[2];
                 _Pragma("unroll UNRF") for (int o = 0; o < nof; o++) {          // branch-free row update
@@ -843,7 +867,11 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             atomicAdd(a.prof + 56 + (mi < 7ull ? mi : 7ull), 1ull);     // waves per loop count
         }
     }
-    if (!cert || !isfinite(J)) {
+    const bool finJ = isfinite(J);
+    // fp32 pass of a refined request: a certified robot goes on, with its sets, to the fp64
+    // refinement pass (a.refine), which writes the outputs
+    const bool to_refine = a.refine && cert && finJ;
+    if (!cert || !finJ || to_refine) {
         if constexpr (PR == 2) {           // the pair's combined row flags (bit o = obstacle o)
 #pragma unroll
             for (int i = 0; i < (N + 1) / 2; i++) {
@@ -855,22 +883,26 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         // the next stage takes over: one atomic per wave for the lanes here (exec mask), each
         // lane's slot from its rank among them (per-lane atomics on the one counter serialise:
         // a first pass hands on ~21k robots at once)
-        const uint64_t m = __builtin_amdgcn_read_exec();
-        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        int base = 0;
-        if (rank == 0) base = atomicAdd(a.retry_count, (int)__popcll(m));
-        const int slot = __builtin_amdgcn_readfirstlane(base) + rank;
-        a.retry[slot] = (int32_t)b;
-        if (a.retry_sets) {                                   // ... from this active set
-            // slot-minor record (word w at retry_sets[w * B + slot]): a wave's consecutive
-            // slots make each word one coalesced store
-            uint32_t *ws = a.retry_sets + slot;
+        auto hand_on = [&](int32_t *list, int32_t *count, uint32_t *sets) __attribute__((always_inline)) {
+            const uint64_t m = __builtin_amdgcn_read_exec();
+            const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            int base = 0;
+            if (rank == 0) base = atomicAdd(count, (int)__popcll(m));
+            const int slot = __builtin_amdgcn_readfirstlane(base) + rank;
+            list[slot] = (int32_t)b;
+            if (sets) {                                       // ... from this active set
+                // slot-minor record (word w at sets[w * B + slot]): a wave's consecutive
+                // slots make each word one coalesced store
+                uint32_t *ws = sets + slot;
 #pragma unroll
-            for (int k = 0; k < N; k++) ws[k * a.B] = Hf.get(k);
+                for (int k = 0; k < N; k++) ws[k * a.B] = Hf.get(k);
 #pragma unroll
-            for (int j = 0; j < NB; j++) ws[(N + j) * a.B] = Bf.get(j);
-            ws[(N + NB) * a.B] = (uint32_t)it;
-        }
+                for (int j = 0; j < NB; j++) ws[(N + j) * a.B] = Bf.get(j);
+                ws[(N + NB) * a.B] = (uint32_t)it;
+            }
+        };
+        if (to_refine) hand_on(a.refine, a.refine_count, a.refine_sets);
+        else hand_on(a.retry, a.retry_count, a.retry_sets);
         if (a.prof) atomicMax(a.prof + 23, __builtin_amdgcn_s_memtime() - t_entry);   // longest lane, entry to exit
         return;
     }
@@ -981,10 +1013,17 @@ using namespace rmpc;
 #undef PY
 #undef V1
 
-bool rmpc_mpc_fast_supported(int N, int bs, int prec, bool lti) {
+bool rmpc_mpc_fast_supported(int N, int bs, int prec, bool lti, int no) {
     if (lti) return prec != RMPC_F32 && (N == 6 || N == 10 || N == 20);   // LTI: block size unused
     if (prec == RMPC_F32) return bs == 1 && (N == 20 || N == 30);
+    // fp64 N = 30: the paired-lane 8-obstacle instance (BASELINE config 4's shape) only
+    // (RMPC_NO_F64_N30=1: the lane-group path from a cold start, the round-2 route; A/B)
+    if (bs == 1 && N == 30) return no == 8 && !rmpc_knob("RMPC_NO_F64_N30");
     return (bs == 1 && (N == 6 || N == 10 || N == 20)) || (bs == 2 && N == 6);
+}
+
+bool rmpc_mpc_refine_supported(int N, int bs, int no) {
+    return bs == 1 && ((N == 30 && no == 8) || N == 20);
 }
 
 hipError_t rmpc_launch_mpc_fast(const MpcFastArgs &a, int N, int bs, int prec, hipStream_t stream, bool lti) {
@@ -992,9 +1031,11 @@ hipError_t rmpc_launch_mpc_fast(const MpcFastArgs &a, int N, int bs, int prec, h
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + RMPC_WAVE - 1) / RMPC_WAVE)), block(RMPC_WAVE);
     // + the setup's staging scratch (64 robots x 17 doubles): 39.8 KB per wave at N = 20 in fp64,
-    // so four waves still share a CU
+    // so four waves still share a CU.  Paired lanes: 32 robot columns, no staging (fp64 N = 30:
+    // 23 KB per wave)
     const size_t lds = (size_t)3 * N * RMPC_WAVE * (prec == RMPC_F32 ? sizeof(float) : sizeof(double)) +
                        (size_t)RMPC_WAVE * 17 * sizeof(double);
+    const size_t lds2 = (size_t)3 * N * (RMPC_WAVE / 2) * (prec == RMPC_F32 ? sizeof(float) : sizeof(double));
     // RMPC_FAST_NOSPEC=1: runtime obstacle loop even where a compile-time instance exists (A/B)
     const char *ns_e = rmpc_knob("RMPC_FAST_NOSPEC");
     const bool nospec = ns_e && *ns_e == '1';
@@ -1010,13 +1051,17 @@ hipError_t rmpc_launch_mpc_fast(const MpcFastArgs &a, int N, int bs, int prec, h
         const char *pr_e = rmpc_knob("RMPC_FAST_PAIR");
         const bool pair = !(pr_e && *pr_e == '0');
         const dim3 grid2((unsigned)((n + RMPC_WAVE / 2 - 1) / (RMPC_WAVE / 2)));
-        if (bs == 1 && N == 30 && a.no == 8 && !nospec && pair) hipLaunchKernelGGL((mpc_ltv_fast_kernel<30, 1, float, false, 8, 2>), grid2, block, lds, stream, a);
+        if (bs == 1 && N == 30 && a.no == 8 && !nospec && pair) hipLaunchKernelGGL((mpc_ltv_fast_kernel<30, 1, float, false, 8, 2>), grid2, block, lds2, stream, a);
         else if (bs == 1 && N == 30 && a.no == 8 && !nospec) hipLaunchKernelGGL((mpc_ltv_fast_kernel<30, 1, float, false, 8>), grid, block, lds, stream, a);
         else if (bs == 1 && N == 30) hipLaunchKernelGGL((mpc_ltv_fast_kernel<30, 1, float, false>), grid, block, lds, stream, a);
         else if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, float, false>), grid, block, lds, stream, a);
         else return hipErrorInvalidValue;
     } else {
-        if (bs == 1 && N == 20 && a.no == 3 && !nospec) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, false, 3>), grid, block, lds, stream, a);
+        const dim3 grid2((unsigned)((n + RMPC_WAVE / 2 - 1) / (RMPC_WAVE / 2)));
+        // (N = 30, 8 obstacles in fp64: paired lanes -- fp64 requests and the fp32 requests'
+        // refinement pass)
+        if (bs == 1 && N == 30 && a.no == 8) hipLaunchKernelGGL((mpc_ltv_fast_kernel<30, 1, double, false, 8, 2>), grid2, block, lds2, stream, a);
+        else if (bs == 1 && N == 20 && a.no == 3 && !nospec) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, false, 3>), grid, block, lds, stream, a);
         else if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, false>), grid, block, lds, stream, a);
         else if (bs == 1 && N == 10) hipLaunchKernelGGL((mpc_ltv_fast_kernel<10, 1, double, false>), grid, block, lds, stream, a);
         else if (bs == 1 && N == 6) hipLaunchKernelGGL((mpc_ltv_fast_kernel<6, 1, double, false>), grid, block, lds, stream, a);

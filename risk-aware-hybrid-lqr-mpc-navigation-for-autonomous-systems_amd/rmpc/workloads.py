@@ -92,6 +92,31 @@ def cfg5_t0(idx, A=2.0, a=0.5, obstacles=DEFAULT_OBS, d_mpc=0.7667):
     return np.where(gi % 2 == 0, near[(gi // 2) % len(near)], far[(gi // 2) % len(far)])
 
 
+def fleet_t0(idx, B_total, fleet=0, fleets=1):
+    """Time offsets of fleet `fleet` of `fleets` independent fleets (bench.py's batches in
+    flight): fleet f is the base workload shifted by f/fleets of the spacing between
+    neighbouring robots, so no two fleets share a reference segment.  Fleet 0 is t0_at."""
+    return (np.asarray(idx, dtype=np.float64) + fleet / max(1, fleets)) / B_total * PERIOD
+
+
+def fleet_seed(seed, fleet=0):
+    """Start-noise seed of fleet `fleet` (fleet 0: the config's own seed)."""
+    return seed + 1000 * fleet
+
+
+def gather_interleaved(dist, local, world, out=None):
+    """SURVEY 8(e)'s batch gather: every rank's round-robin shard `local` ([B, ...], rank r
+    holding global robots r, r + W, ...) all-gathered and interleaved back into global robot
+    order ([W * B, ...]).  One all_gather_into_tensor (RCCL over xGMI on the GPU, gloo on the
+    CPU) into `out` ([W * B, ...], allocated when None), then a transpose of its [W][B] view.
+    Returns (global tensor, out)."""
+    if out is None:
+        out = local.new_empty((world * local.shape[0],) + tuple(local.shape[1:]))
+    dist.all_gather_into_tensor(out, local.contiguous())
+    g = out.view((world, local.shape[0]) + tuple(local.shape[1:])).transpose(0, 1)
+    return g.reshape((-1,) + tuple(local.shape[1:])), out
+
+
 def aggregate(dist, elapsed, counts, device="cpu"):
     """Cross-rank reduction of one bench run (the only collectives of the multi-GPU bench):
     the slowest rank's elapsed time (MAX) and the per-status robot counts (SUM).

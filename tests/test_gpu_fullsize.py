@@ -123,6 +123,65 @@ def test_hybrid_cfg5_tail_robots_vs_device_mpc_iterations(rm, golden, monkeypatc
     assert np.all(d[fx["ok"]] <= 1e-9), d[fx["ok"]].max()
 
 
+def _rel(a, b, axes):
+    """Per-robot relative error max|a - b| / max(1, max|b|) (the north star's "relative
+    control error"; the max(1, .) keeps near-zero controls from dividing by ~0)."""
+    return np.abs(a - b).max(axis=axes) / np.maximum(1.0, np.abs(b).max(axis=axes))
+
+
+@pytest.mark.parametrize("caps", [(0, 0), (14, 6)], ids=["default_caps", "inflight_caps"])
+def test_mpc_cfg4_full_size_fp32_matches_fp64(rm, caps, capsys):
+    """BASELINE config 4 at its own per-GPU size, exactly `bench.py --config cfg4`'s workload:
+    32768 robots, N=30, the union-8 obstacles (run_simulation.py:191-221), fp32 arithmetic,
+    device Figure-8 references at t0 = i/B * period, start noise seed 2, step_count 10; once
+    with the library's default stage caps and once with the bench's in-flight caps (14, 6).
+    Every output the reference returns -- u0, u_seq and x_pred (mpc_controller.py:497-505)
+    -- against the fp64 C port, all robots: relative error <= 1e-4 (north star).  The 50
+    robots with the largest u_seq error also go through the independent exact QP
+    (oracle/qp.py, the QP CVXPY is given)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from rmpc import workloads as W
+    B, N = 32768, 30
+    idx = np.arange(B)
+    xr, ur = rm.batch.figure8_batch(W.t0_at(idx, B), N + 1)
+    x0 = xr[:, 0] + W.noise_at(idx, W.CONFIGS["cfg4"]["seed"])
+    obs = W.UNION8_OBS
+    p = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02,
+                              precision=1)
+    rm.batch.set_stage_caps(*caps)
+    try:
+        out = rm.batch.mpc_solve_batch(p, x0, xr, ur, obs, step_count=np.full(B, 10, np.int32))
+    finally:
+        rm.batch.set_stage_caps(0, 0)
+    cp = cpu.mpc_params(N, (15, 15, 50), (.1, .1), (30, 30, 40), 0.3, 5000., 2., 3., 0.02)
+    ref = cpu.mpc_solve_batch(cp, x0, xr, ur, obs, step_count=np.full(B, 10, np.int32), threads=16)
+    both = (out["status"] == 0) & (ref["status"] == 0)
+    assert both.mean() >= 0.999, np.bincount(out["status"])
+    e_u0 = _rel(out["u0"], ref["u0"], 1)[both]
+    e_us = _rel(out["u_seq"], ref["u_seq"], (1, 2))[both]
+    e_xp = _rel(out["x_pred"], ref["x_pred"], (1, 2))[both]
+    with capsys.disabled():
+        print(f"\n[cfg4 32768 caps {caps}] optimal {both.mean():.5f}; max rel u0 {e_u0.max():.2e} "
+              f"u_seq {e_us.max():.2e} x_pred {e_xp.max():.2e}; iters mean {out['iters'].mean():.2f} "
+              f"max {out['iters'].max()}")
+    assert e_u0.max() <= 1e-4 and e_us.max() <= 1e-4 and e_xp.max() <= 1e-4
+    # the worst robots against the independent exact QP
+    worst = np.where(both)[0][np.argsort(e_us)[-50:]]
+
+    def qp(b):
+        oc = ompc.MPCController(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+        oc._step_count = 10
+        return oc.solve_with_ltv(x0[b], xr[b], ur[b], obs)
+    with ThreadPoolExecutor(8) as ex:
+        sols = list(ex.map(qp, worst))
+    assert all(s.status == "optimal" for s in sols)
+    e_qp = np.array([_rel(out["u_seq"][b], s.control_sequence, (0, 1)) for b, s in zip(worst, sols)])
+    e_qx = np.array([_rel(out["x_pred"][b], s.predicted_states, (0, 1)) for b, s in zip(worst, sols)])
+    with capsys.disabled():
+        print(f"[cfg4 worst 50 vs exact QP] max rel u_seq {e_qp.max():.2e} x_pred {e_qx.max():.2e}")
+    assert e_qp.max() <= 1e-4 and e_qx.max() <= 1e-4
+
+
 # ------------------------------------------------------------------ LQR API gaps (a11)
 def test_lqr_get_lqr_gain_unguarded_and_dt_override(rm):
     """LQRController.get_lqr_gain (lqr_controller.py:217-242): no v_r guard, optional dt

@@ -56,6 +56,20 @@ def test_rank_inputs_equal_global_slices():
         np.testing.assert_array_equal(W.noise_for(lo, hi, 7), full_nz[lo:hi])
 
 
+def test_fleets_in_flight_are_distinct_workloads():
+    """bench.py's batches in flight are independent fleets: fleet 0 is the config's own
+    workload; the others have their own reference offsets and start noise."""
+    B = 65536
+    idx = W.shard_indices(B, 1, 0)
+    np.testing.assert_array_equal(W.fleet_t0(idx, B, 0, 3), W.t0_at(idx, B))
+    assert W.fleet_seed(1, 0) == 1
+    t = [W.fleet_t0(idx, B, f, 3) for f in range(3)]
+    nz = [W.noise_at(idx, W.fleet_seed(1, f)) for f in range(3)]
+    for f in range(1, 3):
+        assert np.all(t[f] > t[f - 1]) and np.all(t[f] < t[0] + W.PERIOD / B)
+        assert not np.any(nz[f] == nz[0])
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -98,8 +112,8 @@ def test_gloo_two_ranks_aggregate():
 
 def _solve_worker(rank, world, port, q):
     """One rank of the bench's multi-GPU path with the C port as the solver: its round-robin
-    shard of a cfg3 batch, solved, then all-gathered and interleaved back into global order
-    exactly as bench.py does after its RCCL all_gather (view(world, B, 2).transpose(0, 1))."""
+    shard of a cfg3 batch, solved, then all-gathered and interleaved back into global order by
+    the function bench.py calls after every timed step (rmpc.workloads.gather_interleaved)."""
     import torch
     import torch.distributed as dist
     from oracle import cpu, figure8
@@ -112,10 +126,11 @@ def _solve_worker(rank, world, port, q):
     p = cpu.mpc_params(N, (15, 15, 50), (.1, .1), (30, 30, 40), 0.3, 5000., 2., 3., 0.02)
     out = cpu.mpc_solve_batch(p, x0, xr, ur, W.DEFAULT_OBS, step_count=np.full(idx.size, 10, np.int32))
     u0 = torch.from_numpy(out["u0"])
-    g = [torch.empty_like(u0) for _ in range(world)]
-    dist.all_gather(g, u0)
-    u0_global = torch.stack(g).transpose(0, 1).reshape(-1, 2).numpy()
-    q.put((rank, u0_global))
+    # the bench's own gather (rmpc.workloads.gather_interleaved, called by bench.py per step)
+    g, buf = W.gather_interleaved(dist, u0, world)
+    assert buf.shape == (B_total, 2)
+    assert torch.equal(g[rank::world], u0)
+    q.put((rank, g.numpy().copy()))
     dist.barrier()
     dist.destroy_process_group()
 
