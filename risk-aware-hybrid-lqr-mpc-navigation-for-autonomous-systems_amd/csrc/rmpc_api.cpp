@@ -578,7 +578,8 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         // tail: the lane-group Riccati kernel (default) or the condensed wave-per-robot one
         // (RMPC_TAIL=dense); RMPC_DISABLE_DENSE skips the tail stage altogether
         const char *tail = rmpc_knob("RMPC_TAIL");
-        const bool use_dense = tail && !strcmp(tail, "dense") && !lti;   // the dense tail is LTV-only
+        const bool use_dense = tail && !strcmp(tail, "dense") && !lti &&   // the dense tail is LTV-only
+                               rmpc_mpc_dense_supported(p->horizon, bs, n_obs);   // (and built: make DENSE=1)
         // tail PDAS cap before projected Newton (sweeps: 4 at N <= 20, 6 beyond -- config 4)
         const int tail_cap = rmpc_knob("RMPC_DENSE_CAP") ? atoi(rmpc_knob("RMPC_DENSE_CAP"))
                              : c->tail_cap > 0          ? c->tail_cap
@@ -677,6 +678,19 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
     }
     return RMPC_OK;
 }
+
+#if !RMPC_WITH_DENSE
+// The condensed wave-per-robot MFMA tail (csrc/rmpc_mpc_dense.hip, RMPC_TAIL=dense) is an A/B
+// alternative that no default path reaches: it is compiled only by `make DENSE=1`.
+bool rmpc_mpc_dense_supported(int, int, int) { return false; }
+hipError_t rmpc_launch_mpc_dense_f64(const MpcDevParams &, int, int, int, int64_t, const double *, const double *,
+                                     int, const double *, int, const double *, int32_t *, double *, double *,
+                                     double *, double *, int32_t *, uint8_t *, int32_t *, const int32_t *,
+                                     const int32_t *, int32_t *, int32_t *, int32_t *, int, const uint32_t *,
+                                     hipStream_t, unsigned long long *) {
+    return hipErrorInvalidValue;
+}
+#endif
 
 // stage a host array to the device (returns device pointer or nullptr when src is null)
 template <typename T>

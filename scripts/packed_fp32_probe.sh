@@ -1,0 +1,61 @@
+#!/bin/bash
+# Root-cause probe for the round-2 packed-fp32 wrong-result defect.
+#
+# Builds, HERE (no GPU needed), variants of librmpc from a given commit's sources into
+# probe/ (git-ignored .so files, which travel to the GPU box):
+#   noslp       -fno-slp-vectorize (the round-2 fix; no packed fp32)
+#   slp         the SLP vectorizer on (packed fp32 v_pk_* code), as hipcc builds it
+#   asis        slp, but the fast kernel's device code round-tripped through its assembly
+#               unchanged (control for the edited variants below)
+#   nop_after   asis + `s_nop 1` after every v_pk_* instruction of the fast kernel
+#   nop_before  asis + `s_nop 1` before every v_pk_* instruction
+#   wait_before asis + `s_waitcnt vmcnt(0) lgkmcnt(0)` before every v_pk_* instruction
+# Then on the GPU: scripts/debug_fp32_n20.py with RMPC_LIB_PATH=probe/librmpc_<v>.so
+# (RMPC_NO_REFINE=1 so the fp32 pass writes its own outputs).
+#
+# Usage: bash scripts/packed_fp32_probe.sh [commit]   (default 83d8eda, the commit that
+# added -fno-slp-vectorize: its sources are the failing ones when built without it)
+set -e
+REPO=$(cd "$(dirname "$0")/.." && pwd)
+COMMIT=${1:-83d8eda}
+OUT=$REPO/probe
+W=/tmp/rmpc_probe_$COMMIT
+PKG=risk-aware-hybrid-lqr-mpc-navigation-for-autonomous-systems_amd
+LLVM=/opt/rocm/lib/llvm/bin
+FL="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-result"
+mkdir -p "$OUT"
+rm -rf "$W" && mkdir -p "$W/src"
+git -C "$REPO" archive "$COMMIT" include $PKG/csrc $PKG/Makefile | tar -x -C "$W/src"
+cd "$W/src/$PKG"
+make -s -j8 BUILD=build_noslp HIPFLAGS="$FL -fno-slp-vectorize" LIB="$OUT/librmpc_noslp.so"
+make -s -j8 BUILD=build_slp HIPFLAGS="$FL" LIB="$OUT/librmpc_slp.so"
+OTHERS=$(ls build_slp/*.o | grep -v rmpc_mpc_fast)
+F=csrc/rmpc_mpc_fast.hip
+/opt/rocm/bin/hipcc $FL -x hip --cuda-device-only -S $F -o "$W/dev.s"
+for v in asis nop_after nop_before wait_before; do
+    python3 - "$W/dev.s" "$W/dev_$v.s" "$v" <<'EOF'
+import re, sys
+src, dst, mode = sys.argv[1:]
+out, n = [], 0
+for ln in open(src):
+    pk = re.match(r"\s+v_pk_\w+\s", ln) is not None
+    if pk and mode == "nop_before":
+        out.append("\ts_nop 1\n"); n += 1
+    if pk and mode == "wait_before":
+        out.append("\ts_waitcnt vmcnt(0) lgkmcnt(0)\n"); n += 1
+    out.append(ln)
+    if pk and mode == "nop_after":
+        out.append("\ts_nop 1\n"); n += 1
+open(dst, "w").writelines(out)
+print(mode, "inserted", n)
+EOF
+    $LLVM/clang -target amdgcn-amd-amdhsa -mcpu=gfx950 -c "$W/dev_$v.s" -o "$W/dev_$v.o"
+    $LLVM/lld -flavor gnu -m elf64_amdgpu --no-undefined -shared -o "$W/dev_$v.out" "$W/dev_$v.o"
+    $LLVM/clang-offload-bundler -type=o -bundle-align=4096 \
+        -targets=host-x86_64-unknown-linux-gnu,hipv4-amdgcn-amd-amdhsa--gfx950 \
+        -input=/dev/null -input="$W/dev_$v.out" -output="$W/dev_$v.hipfb"
+    /opt/rocm/bin/hipcc $FL -x hip --cuda-host-only -Xclang -fcuda-include-gpubinary -Xclang "$W/dev_$v.hipfb" \
+        -c $F -o "$W/fast_$v.o"
+    /opt/rocm/bin/hipcc $FL -shared -o "$OUT/librmpc_$v.so" "$W/fast_$v.o" $OTHERS
+done
+ls -la "$OUT"

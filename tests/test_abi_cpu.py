@@ -83,6 +83,55 @@ def test_context_without_device_fails_loudly(lib):
         n.context(0)
 
 
+LLVM_BIN = "/opt/rocm/lib/llvm/bin"
+
+
+def gfx950_code_objects(so_path, tmp_path):
+    """The gfx950 code objects embedded in a HIP shared library: its .hip_fatbin section holds
+    one clang offload bundle per translation unit (magic, entry count, then per entry offset,
+    size, target-triple length and triple)."""
+    import struct
+    sec = tmp_path / "fatbin.bin"
+    subprocess.run([f"{LLVM_BIN}/llvm-objcopy", "--dump-section", f".hip_fatbin={sec}", so_path,
+                    str(tmp_path / "stripped.so")], check=True)
+    b = sec.read_bytes()
+    magic, pos, out = b"__CLANG_OFFLOAD_BUNDLE__", 0, []
+    while (i := b.find(magic, pos)) >= 0:
+        n, q = struct.unpack_from("<Q", b, i + 24)[0], i + 32
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", b, q)
+            triple = b[q + 24: q + 24 + tl].decode()
+            q += 24 + tl
+            if triple.endswith("gfx950"):
+                out.append(b[i + off: i + off + size])
+        pos = i + 1
+    return out
+
+
+def test_library_has_no_packed_fp32_code(lib, tmp_path):
+    """The shipped library holds no packed-fp32 (VOP3P v_pk_{fma,mul,add}_f32) instructions.
+    In round 2 an fp32 build with packed code certified wrong controls for 29-32 of 2048 robots
+    (lanes 12-15 of lane rows 1-3) depending on the instruction schedule; the library is built
+    with -fno-slp-vectorize -fno-vectorize, the two passes that emitted packed fp32 (the
+    Makefile).  This guards against a toolchain update or a code change
+    bringing such code back unnoticed."""
+    if not os.path.exists(f"{LLVM_BIN}/llvm-objdump"):
+        pytest.skip("no llvm-objdump")
+    from rmpc import _native
+    cos = gfx950_code_objects(_native.LIB_PATH, tmp_path)
+    assert len(cos) >= 4                          # one per device translation unit
+    found = {}
+    for k, co in enumerate(cos):
+        f = tmp_path / f"co{k}.elf"
+        f.write_bytes(co)
+        dis = subprocess.run([f"{LLVM_BIN}/llvm-objdump", "-d", "--mcpu=gfx950", str(f)], check=True,
+                             capture_output=True, text=True).stdout
+        assert "mpc_" in dis or "lqr_" in dis or "kernel" in dis
+        for m in re.findall(r"\bv_pk_(?:fma|mul|add)_f32\b", dis):
+            found[m] = found.get(m, 0) + 1
+    assert not found, found
+
+
 def test_params_yaml_surface():
     from rmpc import params
     cfg = params.load_params(os.path.join(GOLDEN, "params.yaml"))

@@ -372,7 +372,10 @@ def test_mpc_tail_only_full_batch(rm, monkeypatch, tail):
     monkeypatch.setenv("RMPC_DIAG", "1")   # knobs are read in diagnostics mode only
     monkeypatch.setenv("RMPC_FAST_CAP", "0")
     if tail == "dense":
-        monkeypatch.setenv("RMPC_DIAG", "1")   # knobs are read in diagnostics mode only
+        # the condensed MFMA tail is an A/B alternative built only by `make DENSE=1`
+        with open(rm._native.LIB_PATH, "rb") as f:
+            if b"mpc_dense_kernel" not in f.read():
+                pytest.skip("library built without the dense tail (make DENSE=1)")
         monkeypatch.setenv("RMPC_TAIL", "dense")
     B, N = 65536, 20
     t0 = (np.arange(B) / B) * (2 * np.pi / 0.5)
