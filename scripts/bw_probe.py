@@ -3,7 +3,7 @@ batch (the same difficulty mix at every size) and report, per size, the stage ti
 fast kernel's per-wave cycles per PDAS iteration (RMPC_DENSE_PROF=1).  If the per-iteration
 cycles grow with the number of concurrently running waves, the waves contend for the memory
 system (the 64 B/step/iteration gain rows spill out of L2).
-Usage: RMPC_DIAG=1 python scripts/r02_bw_probe.py [sizes...]"""
+Usage: RMPC_DIAG=1 python scripts/bw_probe.py [sizes...]"""
 import json
 import os
 import subprocess

@@ -1,22 +1,34 @@
 #!/bin/bash
-# One measurement session on the GPU box: PMC HBM passes -> traffic json (read by bench.py via
-# profiles/<round>/pmc_traffic.json) -> default bench line -> other configs -> rocprofv3 stats.
-# Stops at the first failing GPU step.  Usage: bash scripts/measure_round.sh <tag> <round-dir>
-cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
-tag=${1:-v}; rdir=${2:-profiles/r01}
-set -o pipefail
-step() { echo "== $*" | tee -a gpurun_out/progress_$tag.log; }
-step pmc
-bash scripts/pmc_hbm.sh ${tag}_hbm > gpurun_out/${tag}_pmc.log 2>&1 || exit $?
+# Measurement session of a round on the GPU box (stops at the first failing GPU step):
+# PMC HBM passes -> pmc_traffic.json, PMC fp64-VALU passes -> pmc_flops.json (both read by
+# bench.py from profiles/), bench lines for every BASELINE configuration, rocprofv3 stats.
+# Usage: bash scripts/measure_round.sh <tag> <profiles dir>   (outputs under gpurun_out/<tag>_*;
+# the PMC jsons are copied into the profiles dir, where bench.py finds the newest)
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
+tag=${1:-m}; rdir=${2:-profiles/r03}
+mkdir -p gpurun_out $rdir
+step() { echo "== $(date +%T) $*"; }
+step pmc hbm
+bash scripts/pmc_hbm.sh ${tag}_hbm > gpurun_out/${tag}_pmc_hbm.log 2>&1 || { tail gpurun_out/${tag}_pmc_hbm.log; exit 1; }
 cp gpurun_out/${tag}_hbm_traffic.json $rdir/pmc_traffic.json
+step pmc flops
+bash scripts/pmc_flops.sh ${tag}_fl > gpurun_out/${tag}_pmc_flops.log 2>&1 || { tail gpurun_out/${tag}_pmc_flops.log; exit 1; }
+cp gpurun_out/${tag}_fl_flops.json $rdir/pmc_flops.json
 step bench cfg3
-timeout -k 10 600 python bench.py --steps 20 --warmup 3 > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || exit $?
+timeout -k 10 600 python bench.py > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || { tail gpurun_out/${tag}_bench.err; exit 1; }
 for c in cfg2 cfg4 cfg5; do
   step bench $c
-  timeout -k 10 300 python bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/${tag}_bench_$c.json 2> gpurun_out/${tag}_bench_$c.err || exit $?
+  timeout -k 10 400 python bench.py --config $c --no-pcie > gpurun_out/${tag}_bench_$c.json 2> gpurun_out/${tag}_bench_$c.err || { tail gpurun_out/${tag}_bench_$c.err; exit 1; }
 done
 step bench lti
-timeout -k 10 300 python bench.py --lti --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/${tag}_bench_lti.json 2> gpurun_out/${tag}_bench_lti.err || exit $?
+timeout -k 10 300 python bench.py --lti --no-cpu-baseline --no-pcie > gpurun_out/${tag}_bench_lti.json 2> gpurun_out/${tag}_bench_lti.err || exit 1
 step rocprof
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/${tag}_prof_bench.json 2> gpurun_out/${tag}_prof.err || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pcie > gpurun_out/${tag}_prof_bench.json 2> gpurun_out/${tag}_prof.err || exit 1
+step rocprof one batch in flight
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof1 -o run --output-format csv -- python3 bench.py --inflight 1 --steps 10 --warmup 2 --no-cpu-baseline --no-pcie > gpurun_out/${tag}_prof1_bench.json 2> gpurun_out/${tag}_prof1.err || exit 1
+step bench cfg3 two in flight
+timeout -k 10 300 python bench.py --inflight 2 --no-cpu-baseline --no-pcie > gpurun_out/${tag}_bench_inflight2.json 2> gpurun_out/${tag}_bench_inflight2.err || exit 1
+step smoke
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 || { cat gpurun_out/${tag}_smoke.log; exit 1; }
 step done
+for f in gpurun_out/${tag}_bench*.json; do python -c "import json,sys;d=json.load(open('$f'));r=d.get('roofline') or {};print('$f', '%.4e'%d['value'], d['unit'], 'ms %.4f'%d['ms_per_step'], 'frac', r.get('frac'), 'frac_exec', r.get('frac_executed'), 'cpu', (d.get('cpu_baseline') or {}).get('value'))"; done
