@@ -78,7 +78,7 @@ struct RmpcCtx {
     DevBuf stage[SB_COUNT];    // staging buffers for host-pointer entry points
     DevBuf idx_lqr, idx_mpc, counts, hyb_status;
     DevBuf fast_gains, retry, retry2, retry_count, prof, retry_sets;
-    DevBuf retry_a, retry_sets_a;   // two-pass fast stage: the first pass's list and sets
+    DevBuf retry_a, retry_sets_a, retry_b, retry_sets_b;   // multi-pass fast stage: ping-pong lists and sets
     DevBuf refine, refine_sets;     // fp32 requests: the fp32-certified robots and their sets
     GroupDiag gdiag;           // lane-group tail diagnostics (RMPC_GROUP_CHECK, RMPC_DENSE_PROF=2)
     // closed-loop rollout state (rmpc_rollout_batch)
@@ -244,6 +244,8 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     c->retry_sets.release();
     c->retry_a.release();
     c->retry_sets_a.release();
+    c->retry_b.release();
+    c->retry_sets_b.release();
     c->refine.release();
     c->refine_sets.release();
     for (DevBuf *d : {&c->ro_x, &c->ro_xr, &c->ro_ur, &c->ro_u, &c->ro_step, &c->ro_cache, &c->ro_prev,
@@ -505,6 +507,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                      : c->fast_cap > 0        ? c->fast_cap
                                               : (p->horizon <= 20 ? (lti ? 9 : 7) : 12);
         const bool warm = !rmpc_knob("RMPC_COLD_TAIL");
+        a.init_zc = rmpc_knob("RMPC_INIT_ZC") ? atoi(rmpc_knob("RMPC_INIT_ZC")) : 0;
         if (warm) {
             HIP_TRY(c->retry_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
             a.retry_sets = (uint32_t *)c->retry_sets.p;
@@ -519,16 +522,25 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             HIP_TRY(hipMemsetAsync(pc, 0, 64 * sizeof(unsigned long long), s));
         }
         a.prof = pc;
-        // Two passes over the lane-per-robot kernel (large batches, warm-started tail): the first
-        // runs every robot for `split` PDAS iterations (most certify in the first: 67% at
-        // BASELINE config 3), the second continues only the uncertified ones, compacted into
-        // dense waves, from their sets (MpcFastArgs::warm_sets), up to the stage cap.  A
-        // robot's iterate path is the one-pass path; what changes is that its second-pass
-        // wave holds no robot that has already finished, so the long waves are a third as
-        // many and run on a chip no longer crowded by the short ones.
-        // (RMPC_FAST_SPLIT=<first-pass cap>, A/B only; default 0 = one pass: measured slower)
-        const int split = rmpc_knob("RMPC_FAST_SPLIT") ? atoi(rmpc_knob("RMPC_FAST_SPLIT")) : 0;
-        const bool two_pass = warm && split > 0 && split < a.pdas_cap && B >= 8192;
+        // Multi-pass lane-per-robot stage (large batches, warm-started tail): pass i runs the
+        // robots the previous pass handed on for up to caps[i] PDAS solves in total, compacted
+        // into dense waves and continued from their sets (MpcFastArgs::warm_sets); the last pass
+        // runs up to the stage cap and hands on to the tail.  A robot's iterate path is the
+        // one-pass path (the cycle history resumes from the sets' signature); what changes is
+        // that a later pass's wave holds no robot that has already finished: at BASELINE
+        // config 3, 67% of the robots certify in their first solve, but a 64-robot wave almost
+        // always holds one that needs 3-7.  (RMPC_FAST_SPLIT=c1[,c2[,c3]]: the earlier passes'
+        // caps, A/B only; default one pass)
+        int splits[3], nsplit = 0;
+        if (const char *sp = rmpc_knob("RMPC_FAST_SPLIT")) {
+            for (const char *q = sp; *q && nsplit < 3;) {
+                const int v = atoi(q);
+                if (v > (nsplit ? splits[nsplit - 1] : 0) && v < a.pdas_cap) splits[nsplit++] = v;
+                while (*q && *q != ',') q++;
+                if (*q == ',') q++;
+            }
+        }
+        if (!warm || B < 8192) nsplit = 0;
         // Mixed precision for fp32 requests (BASELINE config 4): the fp32 lane-per-robot pass
         // only finds the active sets.  Every robot it certifies goes on, with its sets, to an
         // fp64 pass of the same kernel that re-solves the equality-constrained QP of those sets
@@ -536,7 +548,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         // `extra_cap` solves); it writes the outputs, which are therefore fp64-exact.  What it
         // does not certify joins the fp64 tail's list.  (RMPC_NO_REFINE=1: the fp32 pass writes
         // its own outputs, the round-2 behaviour; A/B only)
-        const bool refine = f32 && warm && !two_pass && rmpc_mpc_refine_supported(p->horizon, bs, n_obs) &&
+        const bool refine = f32 && warm && rmpc_mpc_refine_supported(p->horizon, bs, n_obs) &&
                             !rmpc_knob("RMPC_NO_REFINE");
         if (refine) {
             HIP_TRY(c->refine.ensure((size_t)B * sizeof(int32_t)));
@@ -546,19 +558,23 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             a.refine_sets = (uint32_t *)c->refine_sets.p;
         }
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[0], s));
-        if (two_pass) {
-            HIP_TRY(c->retry_a.ensure((size_t)B * sizeof(int32_t)));
-            HIP_TRY(c->retry_sets_a.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
-            MpcFastArgs a1 = a;            // pass 1: every robot, `split` iterations -> list A
-            a1.pdas_cap = split;
-            a1.retry = (int32_t *)c->retry_a.p;
-            a1.retry_count = cnt + 4;
-            a1.retry_sets = (uint32_t *)c->retry_sets_a.p;
-            HIP_TRY(rmpc_launch_mpc_fast(a1, p->horizon, bs, p->precision, s, lti));
-            dbg_sync(s, "fast pass 1");
-            a.index = a1.retry;            // pass 2: list A, from its sets -> the tail's list
-            a.count = a1.retry_count;
-            a.warm_sets = a1.retry_sets;
+        {
+            DevBuf *lists[2] = {&c->retry_a, &c->retry_b}, *sets[2] = {&c->retry_sets_a, &c->retry_sets_b};
+            int32_t *pass_cnt[3] = {cnt + 2, cnt + 3, cnt + 5};
+            for (int i = 0; i < nsplit; i++) {
+                HIP_TRY(lists[i % 2]->ensure((size_t)B * sizeof(int32_t)));
+                HIP_TRY(sets[i % 2]->ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
+                MpcFastArgs ai = a;        // pass i: -> list i % 2 with its sets
+                ai.pdas_cap = splits[i];
+                ai.retry = (int32_t *)lists[i % 2]->p;
+                ai.retry_count = pass_cnt[i];
+                ai.retry_sets = (uint32_t *)sets[i % 2]->p;
+                HIP_TRY(rmpc_launch_mpc_fast(ai, p->horizon, bs, p->precision, s, lti));
+                dbg_sync(s, "fast pass");
+                a.index = ai.retry;        // the next pass: that list, from its sets
+                a.count = ai.retry_count;
+                a.warm_sets = ai.retry_sets;
+            }
         }
         HIP_TRY(rmpc_launch_mpc_fast(a, p->horizon, bs, p->precision, s, lti));
         if (refine) {

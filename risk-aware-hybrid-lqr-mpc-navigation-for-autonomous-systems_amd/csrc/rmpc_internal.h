@@ -75,6 +75,7 @@ struct MpcFastArgs {
     // outputs; uncertified ones still go to `retry`
     int32_t *refine, *refine_count;
     uint32_t *refine_sets;
+    int init_zc;                     // cold start: hinge rows violated by the free response start active
 };
 // list counters per set of a context (retry_count holds two sets, used by alternate calls)
 #define RMPC_COUNT_WORDS 16
