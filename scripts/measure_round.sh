@@ -1,13 +1,21 @@
 #!/bin/bash
 # Measurement session of a round on the GPU box (stops at the first failing GPU step):
 # PMC HBM passes -> pmc_traffic.json, PMC fp64-VALU passes -> pmc_flops.json (both read by
-# bench.py from profiles/), bench lines for every BASELINE configuration, rocprofv3 stats.
+# bench.py from profiles/), bench lines for every BASELINE configuration, rocprofv3 kernel
+# stats of config 3 (three in flight and one batch), config 4 (fp32 pass + fp64 refinement +
+# tail) and config 5 (decide + LQR + MPC branch), smoke.
 # Usage: bash scripts/measure_round.sh <tag> <profiles dir>   (outputs under gpurun_out/<tag>_*;
 # the PMC jsons are copied into the profiles dir, where bench.py finds the newest)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
 tag=${1:-m}; rdir=${2:-profiles/r03}
 mkdir -p gpurun_out $rdir
 step() { echo "== $(date +%T) $*"; }
+prof() {   # prof <name> <bench args...>: rocprofv3 kernel trace + stats of a short bench run
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof_$name -o run --output-format csv \
+    -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pcie "$@" \
+    > gpurun_out/${tag}_prof_${name}_bench.json 2> gpurun_out/${tag}_prof_$name.err || { tail gpurun_out/${tag}_prof_$name.err; exit 1; }
+}
 step pmc hbm
 bash scripts/pmc_hbm.sh ${tag}_hbm > gpurun_out/${tag}_pmc_hbm.log 2>&1 || { tail gpurun_out/${tag}_pmc_hbm.log; exit 1; }
 cp gpurun_out/${tag}_hbm_traffic.json $rdir/pmc_traffic.json
@@ -23,12 +31,11 @@ done
 step bench lti
 timeout -k 10 300 python bench.py --lti --no-cpu-baseline --no-pcie > gpurun_out/${tag}_bench_lti.json 2> gpurun_out/${tag}_bench_lti.err || exit 1
 step rocprof
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pcie > gpurun_out/${tag}_prof_bench.json 2> gpurun_out/${tag}_prof.err || exit 1
-step rocprof one batch in flight
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof1 -o run --output-format csv -- python3 bench.py --inflight 1 --steps 10 --warmup 2 --no-cpu-baseline --no-pcie > gpurun_out/${tag}_prof1_bench.json 2> gpurun_out/${tag}_prof1.err || exit 1
-step bench cfg3 two in flight
-timeout -k 10 300 python bench.py --inflight 2 --no-cpu-baseline --no-pcie > gpurun_out/${tag}_bench_inflight2.json 2> gpurun_out/${tag}_bench_inflight2.err || exit 1
+prof cfg3_inflight3
+prof cfg3_inflight1 --inflight 1
+prof cfg4_inflight1 --config cfg4 --inflight 1
+prof cfg5_inflight1 --config cfg5 --inflight 1
 step smoke
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 || { cat gpurun_out/${tag}_smoke.log; exit 1; }
 step done
-for f in gpurun_out/${tag}_bench*.json; do python -c "import json,sys;d=json.load(open('$f'));r=d.get('roofline') or {};print('$f', '%.4e'%d['value'], d['unit'], 'ms %.4f'%d['ms_per_step'], 'frac', r.get('frac'), 'frac_exec', r.get('frac_executed'), 'cpu', (d.get('cpu_baseline') or {}).get('value'))"; done
+for f in gpurun_out/${tag}_bench*.json; do python -c "import json,sys;d=json.load(open('$f'));r=d.get('roofline') or {};print('$f', '%.4e'%d['value'], d['unit'], 'alone %.4e'%d.get('value_one_batch_alone',0), 'ms %.4f'%d['ms_per_step'], 'frac', r.get('frac'), 'frac_exec', r.get('frac_executed'), 'cpu', (d.get('cpu_baseline') or {}).get('value'))"; done
