@@ -517,9 +517,9 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         const bool prof = rmpc_knob("RMPC_DENSE_PROF") != nullptr;
         unsigned long long *pc = nullptr;
         if (prof) {
-            HIP_TRY(c->prof.ensure(64 * sizeof(unsigned long long)));
+            HIP_TRY(c->prof.ensure(128 * sizeof(unsigned long long)));   // [64..127]: the refinement pass
             pc = (unsigned long long *)c->prof.p;
-            HIP_TRY(hipMemsetAsync(pc, 0, 64 * sizeof(unsigned long long), s));
+            HIP_TRY(hipMemsetAsync(pc, 0, 128 * sizeof(unsigned long long), s));
         }
         a.prof = pc;
         // Multi-pass lane-per-robot stage (large batches, warm-started tail): pass i runs the
@@ -584,7 +584,11 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             r.index = a.refine;
             r.count = a.refine_count;
             r.warm_sets = a.refine_sets;
-            r.extra_cap = rmpc_knob("RMPC_REFINE_CAP") ? atoi(rmpc_knob("RMPC_REFINE_CAP")) : 4;
+            // one fp64 solve from the fp32 sets: the robots whose sets it does not certify go
+            // to the fp64 tail (config 4: 36.5M against 34.8M solves/s with 4 more solves here,
+            // whose slowest waves set the pass's length)
+            r.extra_cap = rmpc_knob("RMPC_REFINE_CAP") ? atoi(rmpc_knob("RMPC_REFINE_CAP")) : 1;
+            r.prof = pc ? pc + 64 : nullptr;   // (diagnostics: the refinement pass's own counters)
             HIP_TRY(rmpc_launch_mpc_fast(r, p->horizon, bs, RMPC_F64, s, lti));
         }
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[1], s));
@@ -632,6 +636,17 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                 fprintf(stderr, "[fast] waves by loop count 0..7+:");
                 for (int q = 56; q < 64; q++) fprintf(stderr, " %llu", h[q]);
                 fprintf(stderr, " | setup %.0f per wave, longest lane entry-to-exit %llu\n", h[22] / w, h[23]);
+                if (refine) {
+                    unsigned long long g[64];
+                    HIP_TRY(hipMemcpy(g, pc + 64, sizeof(g), hipMemcpyDeviceToHost));
+                    const double w2 = g[20] ? (double)g[20] : 1.0, i2 = g[18] ? (double)g[18] : 1.0;
+                    fprintf(stderr, "[refine] waves=%llu per wave: total %.0f back %.0f fwd %.0f iters %.2f setup %.0f | "
+                            "per iter: back %.0f fwd %.0f | slowest wave: total %llu iters %llu | loop counts 0..7+:",
+                            g[20], g[19] / w2, g[16] / w2, g[17] / w2, g[18] / w2, g[22] / w2, g[16] / i2, g[17] / i2,
+                            g[21] >> 16, (g[21] >> 8) & 0xff);
+                    for (int q = 56; q < 64; q++) fprintf(stderr, " %llu", g[q]);
+                    fprintf(stderr, "\n");
+                }
             }
             dbg_sync(s, "group");
             left = (const int32_t *)c->retry2.p;

@@ -310,18 +310,25 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         // switch's MPC branch) and rows from a shared table (rollouts): each 16-lane group
         // addresses its own robot's row.  The staging fills PX/PY/V1 and V0 directly and parks
         // the heading in S[k] for the unwrap / sin-cos loop below.
-        const bool coal = F64 && PR == 1 && (int64_t)(blockIdx.x + 1) * RMPC_WAVE <= n;
+        // (round 3: also the paired-lane and fp32 instances -- a paired wave stages its 32
+        // robots, and fp32 keeps the fp64 heading for the unwrap / sin-cos in TH)
+#ifndef RMPC_COAL_ALL
+#define RMPC_COAL_ALL 1
+#endif
+        constexpr int RW = RMPC_WAVE / PR;                   // robots per wave
+        const bool coal = (F64 ? (PR == 1 || RMPC_COAL_ALL) : RMPC_COAL_ALL) && (int64_t)(blockIdx.x + 1) * RW <= n;
+        double TH[F64 ? 1 : N];                              // fp32: the staged fp64 headings
         if (coal) {
             constexpr int SP = 17;                           // scratch row stride in doubles (bank spread)
             double *const stg = lds_raw + (size_t)3 * N * LW * sizeof(T) / sizeof(double);
-            const int64_t t0 = (int64_t)blockIdx.x * RMPC_WAVE;
+            const int64_t t0 = (int64_t)blockIdx.x * RW;
             const int rr = lane >> 4, ee = lane & 15;
             // all of an array's loads are issued before the first LDS round (one memory latency
             // per array, not per round)
             // robot 4q + rr's first reference row in a shared table, else its robot index
-            int64_t row[16];
+            int64_t row[RW / 4];
 #pragma unroll
-            for (int q = 0; q < 16; q++) {
+            for (int q = 0; q < RW / 4; q++) {
                 const int64_t tq = t0 + 4 * q + rr;
                 const int64_t bq = a.index ? (int64_t)a.index[tq] : tq;
                 row[q] = a.prm.ref_off ? (int64_t)a.prm.ref_off[bq] : bq;
@@ -329,11 +336,11 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             auto stage = [&](const double *src, const int W, const int rows, const int ne, auto put)
                 __attribute__((always_inline)) {
                 constexpr int NP = (3 * N + 15) / 16;        // rounds (sized for x_refs; u_refs uses fewer)
-                double v[NP][16];
+                double v[NP][RW / 4];
 #pragma unroll
                 for (int ps = 0; ps < NP; ps++)
 #pragma unroll
-                    for (int q = 0; q < 16; q++) {
+                    for (int q = 0; q < RW / 4; q++) {
                         const int e = 16 * ps + ee;
                         const int64_t r0 = a.prm.ref_off ? row[q] : row[q] * rows;   // (ref_row0)
                         v[ps][q] = (16 * ps < ne && e < ne) ? src[r0 * W + e] : 0.0;
@@ -343,17 +350,18 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                     if (16 * ps >= ne) break;
                     __syncthreads();
 #pragma unroll
-                    for (int q = 0; q < 16; q++) stg[(4 * q + rr) * SP + ee] = v[ps][q];
+                    for (int q = 0; q < RW / 4; q++) stg[(4 * q + rr) * SP + ee] = v[ps][q];
                     __syncthreads();
 #pragma unroll
                     for (int i = 0; i < 16; i++)
-                        if (16 * ps + i < ne) put(16 * ps + i, stg[lane * SP + i]);
+                        if (16 * ps + i < ne) put(16 * ps + i, stg[ll * SP + i]);
                 }
             };
             stage(a.x_refs, 3, a.ref_rows, 3 * N, [&](const int e, const double v) __attribute__((always_inline)) {
                 if (e % 3 == 0) PX(e / 3) = (T)v;
                 else if (e % 3 == 1) PY(e / 3) = (T)v;
-                else S[e / 3] = (T)v;                        // the heading (fp64 only), for the loop below
+                else if constexpr (F64) S[e / 3] = v;        // the heading, for the loop below
+                else TH[e / 3] = v;
             });
             stage(a.u_refs, 2, a.uref_rows, 2 * N, [&](const int e, const double v) __attribute__((always_inline)) {
                 if (e % 2 == 0) V0[e / 2] = (T)v;
@@ -362,7 +370,9 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         }
 #pragma unroll
         for (int k = 0; k < N; k++) {
-            const double th = coal ? (double)S[k] : xr[3 * k + 2];
+            double th;
+            if constexpr (F64) th = coal ? (double)S[k] : xr[3 * k + 2];
+            else th = coal ? TH[k] : xr[3 * k + 2];
             if (k > 0) corr += unwrap_step(prev, th);
             prev = th;
             const double thu = th + corr;
@@ -1072,7 +1082,8 @@ hipError_t rmpc_launch_mpc_fast(const MpcFastArgs &a, int N, int bs, int prec, h
     // 23 KB per wave)
     const size_t lds = (size_t)3 * N * RMPC_WAVE * (prec == RMPC_F32 ? sizeof(float) : sizeof(double)) +
                        (size_t)RMPC_WAVE * 17 * sizeof(double);
-    const size_t lds2 = (size_t)3 * N * (RMPC_WAVE / 2) * (prec == RMPC_F32 ? sizeof(float) : sizeof(double));
+    const size_t lds2 = (size_t)3 * N * (RMPC_WAVE / 2) * (prec == RMPC_F32 ? sizeof(float) : sizeof(double)) +
+                        (size_t)(RMPC_WAVE / 2) * 17 * sizeof(double);
     // RMPC_FAST_NOSPEC=1: runtime obstacle loop even where a compile-time instance exists (A/B)
     const char *ns_e = rmpc_knob("RMPC_FAST_NOSPEC");
     const bool nospec = ns_e && *ns_e == '1';
