@@ -150,6 +150,7 @@ def main():
     x0_h, xr_h, ur_h = fleets[0]["x0_h"], fleets[0]["xr_h"], fleets[0]["ur_h"]
     x0, xr, ur = fleets[0]["x0"], fleets[0]["xr"], fleets[0]["ur"]
     obs = torch.tensor(obs_list, dtype=torch.float64, device=dev).reshape(-1, 3)
+    W.broadcast_shared(dist, obs)          # rank 0's obstacles on every rank (setup, untimed)
 
     def new_out():
         return dict(u0=torch.empty(B, 2, dtype=torch.float64, device=dev),

@@ -104,6 +104,15 @@ def fleet_seed(seed, fleet=0):
     return seed + 1000 * fleet
 
 
+def broadcast_shared(dist, tensor, src=0):
+    """SURVEY 8(e)'s setup collective: the shared read-only solve data (obstacles, weights)
+    broadcast from rank `src` once before the rollout, so every rank solves against the same
+    bits (in place; returns the tensor).  A no-op without a process group."""
+    if dist is not None:
+        dist.broadcast(tensor, src=src)
+    return tensor
+
+
 def gather_interleaved(dist, local, world, out=None):
     """SURVEY 8(e)'s batch gather: every rank's round-robin shard `local` ([B, ...], rank r
     holding global robots r, r + W, ...) all-gathered and interleaved back into global robot

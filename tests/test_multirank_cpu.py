@@ -124,7 +124,11 @@ def _solve_worker(rank, world, port, q):
     xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, W.t0_at(idx, B_total), N + 1)
     x0 = xr[:, 0] + W.noise_at(idx, 1)
     p = cpu.mpc_params(N, (15, 15, 50), (.1, .1), (30, 30, 40), 0.3, 5000., 2., 3., 0.02)
-    out = cpu.mpc_solve_batch(p, x0, xr, ur, W.DEFAULT_OBS, step_count=np.full(idx.size, 10, np.int32))
+    # the shared obstacles from rank 0 (bench.py's setup broadcast); rank 1 starts from zeros
+    obs = torch.tensor(W.DEFAULT_OBS, dtype=torch.float64) if rank == 0 else torch.zeros(3, 3, dtype=torch.float64)
+    W.broadcast_shared(dist, obs)
+    assert obs.tolist() == [list(o) for o in W.DEFAULT_OBS]
+    out = cpu.mpc_solve_batch(p, x0, xr, ur, obs.numpy(), step_count=np.full(idx.size, 10, np.int32))
     u0 = torch.from_numpy(out["u0"])
     # the bench's own gather (rmpc.workloads.gather_interleaved, called by bench.py per step)
     g, buf = W.gather_interleaved(dist, u0, world)
