@@ -692,7 +692,8 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[2], s));
         // what remains is rare (cycling beyond both, non-finite data): LDS generic kernel, in
         // the requested arithmetic (the dense tail between is fp64 for both)
-        if (f32)
+        // (a refined fp32 request stays fp64 here too: every output it returns is the fp64 optimum)
+        if (f32 && !refine)
             HIP_TRY(rmpc_launch_mpc_f32(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
                                         step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
                                         c->ws.p, left, left_n, s, rmpc_mpc_lds_lanes(L), other_counts(c)));

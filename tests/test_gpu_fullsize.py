@@ -182,6 +182,34 @@ def test_mpc_cfg4_full_size_fp32_matches_fp64(rm, caps, capsys):
     assert e_qp.max() <= 1e-4 and e_qx.max() <= 1e-4
 
 
+@pytest.mark.parametrize("cfg,rank", [("cfg4", 7), ("cfg3", 5)])
+def test_mpc_eight_gpu_rank_shard_matches_cpu_port(rm, cfg, rank, capsys):
+    """One rank's shard of the 8-GPU job, exactly as `bench.py --gpus 8` builds it on that
+    rank: global batch 8 x the per-GPU size (config 4: 262144 robots over 8 GPUs, the
+    BASELINE figure; config 3: 524288), robots rank, rank + 8, ... (round-robin), their
+    Figure-8 offsets and start noise keyed on the global index.  The rank's 32768 / 65536
+    robots against the fp64 C port: u0, u_seq, x_pred (fp64-exact: 1e-9 absolute)."""
+    from rmpc import workloads as W
+    c = W.CONFIGS[cfg]
+    N, world = c["N"], 8
+    B_per = 32768 if cfg == "cfg4" else c["B"]
+    idx = W.shard_indices(B_per * world, world, rank)
+    assert idx.size == B_per
+    xr, ur = rm.batch.figure8_batch(W.t0_at(idx, B_per * world), N + 1)
+    x0 = xr[:, 0] + W.noise_at(idx, c["seed"])
+    p = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02,
+                              precision=1 if cfg == "cfg4" else 0)
+    out = rm.batch.mpc_solve_batch(p, x0, xr, ur, c["obs"], step_count=np.full(B_per, 10, np.int32))
+    cp = cpu.mpc_params(N, (15, 15, 50), (.1, .1), (30, 30, 40), 0.3, 5000., 2., 3., 0.02)
+    ref = cpu.mpc_solve_batch(cp, x0, xr, ur, c["obs"], step_count=np.full(B_per, 10, np.int32), threads=16)
+    ok = (out["status"] == 0) & (ref["status"] == 0)
+    assert ok.mean() >= 0.999
+    d = {k: float(np.abs(out[k][ok] - ref[k][ok]).max()) for k in ("u0", "u_seq", "x_pred")}
+    with capsys.disabled():
+        print(f"\n[{cfg} rank {rank}/8, {B_per} robots] optimal {ok.mean():.5f} max |diff| {d}")
+    assert max(d.values()) <= 1e-9, d
+
+
 # ------------------------------------------------------------------ LQR API gaps (a11)
 def test_lqr_get_lqr_gain_unguarded_and_dt_override(rm):
     """LQRController.get_lqr_gain (lqr_controller.py:217-242): no v_r guard, optional dt
