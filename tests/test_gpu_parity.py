@@ -616,6 +616,31 @@ def test_rollout_hybrid_matches_oracle_closed_loop(rm):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["mpc", "hybrid"])
+def test_rollout_fp32_request_is_fp64_exact(rm, mode):
+    """fp32 requests (the fp32 active-set pass + fp64 refinement) inside the device closed
+    loops -- shared-table references, index lists of the hybrid switch's MPC branch -- return
+    the fp64 optimum: 256 robots, N=20, 100 steps, states and controls equal to the fp64
+    request's rollout within 1e-9."""
+    steps = 100
+    starts = (np.arange(256) * 37) % 1000
+    kw = dict(start_index=starts, obstacles=ompc.default_obstacles(), mpc_rate=1)
+    if mode == "hybrid":
+        kw.update(lparams=rm._native.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0),
+                  rparams=rm._native.risk_params())
+    outs = []
+    for prec in (0, 1):
+        mp = rm._native.mpc_params(20, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                                   0.02, precision=prec)
+        outs.append(rm.batch.rollout_batch(mode, steps, mparams=mp, **kw))
+    a, b = outs
+    assert a["mpc_status"][0] > 0 and a["mpc_status"][2] == 0 and b["mpc_status"][2] == 0
+    np.testing.assert_array_equal(a["used_mpc"], b["used_mpc"])
+    np.testing.assert_allclose(b["controls"], a["controls"], atol=1e-9, rtol=0)
+    np.testing.assert_allclose(b["states"], a["states"], atol=1e-9, rtol=0)
+
+
+@pytest.mark.gpu
 def test_rollout_hybrid_predictive_risk_matches_oracle(rm):
     """the switch fed with the last MPC solve's x_pred
     (RmpcRiskParams.use_predicted; compute_predictive_risk, risk_metrics.py:131-171).  Not in
