@@ -635,7 +635,8 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                         h[17] / (double)(h[18] ? h[18] : 1), h[21] >> 16, (h[21] >> 8) & 0xff, h[21] & 0xff);
                 fprintf(stderr, "[fast] waves by loop count 0..7+:");
                 for (int q = 56; q < 64; q++) fprintf(stderr, " %llu", h[q]);
-                fprintf(stderr, " | setup %.0f per wave, longest lane entry-to-exit %llu\n", h[22] / w, h[23]);
+                fprintf(stderr, " | setup %.0f per wave, longest lane entry-to-exit %llu, output pass %.0f per lane\n",
+                        h[22] / w, h[23], h[11] / (double)(h[12] ? h[12] : 1));
                 if (refine) {
                     unsigned long long g[64];
                     HIP_TRY(hipMemcpy(g, pc + 64, sizeof(g), hipMemcpyDeviceToHost));

@@ -960,19 +960,47 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     // that only the deviations carry fp32 rounding.
     // LTI: u = du (no u_ref), x_pred = e + x_ref (absolute), no ramp or step count.
     if (PR == 2 && pp) return;             // paired lanes: lane 2r writes the outputs
+    const unsigned long long t_out0 = a.prof ? __builtin_amdgcn_s_memtime() : 0ull;   // (diagnostics)
     const int sc = (!LTI && a.step_count) ? a.step_count[b] : 0;
     T x0 = d0, x1 = d1, x2 = d2;
     double uc0 = 0, uc1 = 0;
+    // The gains are prefetched PFO blocks ahead, as in the forward sweep.  A block's loads are
+    // issued before the previous steps' output stores, and vmcnt counts loads and stores in
+    // issue order, so a load-use wait never waits for those stores: loading each block at its
+    // own step made every step wait for all earlier stores to complete (round 3: ~106k cycles
+    // per lane for this pass at config 3 under full-chip load).
+#ifndef RMPC_PFO
+#define RMPC_PFO 4
+#endif
+    constexpr int PFO = RMPC_PFO;
+    // x_pred's reference rows (LTV: the heading as given, not unwrapped; fp32 also the
+    // positions) loaded before the first output store, for the same reason
+    double xth[(!LTI && F64) ? N + 1 : 1], xrt0 = 0, xrt1 = 0;
+    if constexpr (!LTI && F64) {
+        if (a.x_pred) {
+#pragma unroll
+            for (int k = 0; k <= N; k++) xth[k] = xr[3 * k + 2];
+            xrt0 = xr[3 * N]; xrt1 = xr[3 * N + 1];
+        }
+    }
+    T go[NB][8];
+#pragma unroll
+    for (int j = 0; j < NB && j < PFO; j++) {
+        if constexpr (PR == 2) gt.ld_pair(j, go[j], pp);
+        else gt.ld(j, go[j]);
+    }
 #pragma unroll
     for (int j = 0; j < NB; j++) {
         T du0, du1;
         const int k0 = j * BS;
         const int k1 = (k0 + BS < N) ? k0 + BS : N;
+        if (j + PFO < NB) {
+            if constexpr (PR == 2) gt.ld_pair(j + PFO, go[j + PFO], pp);
+            else gt.ld(j + PFO, go[j + PFO]);
+        }
         {   // the certified inputs, re-derived from the last backward sweep's gains along the
             // same trajectory (no per-iteration input tile)
-            T g[8];
-            if constexpr (PR == 2) gt.ld_pair(j, g, pp);
-            else gt.ld(j, g);
+            const T *const g = go[j];
             T lo0 = -BIG, hi0 = BIG, lo1 = -BIG, hi1 = BIG;
             if constexpr (LTI) {
                 lo0 = -vmax; hi0 = vmax; lo1 = -omax; hi1 = omax;
@@ -1012,9 +1040,13 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                 double *xp = a.x_pred + ((size_t)b * (N + 1) + k) * 3;
                 if constexpr (LTI) {
                     xp[0] = (double)(x0 + PX(k)); xp[1] = (double)(x1 + PY(k)); xp[2] = (double)(x2 + V1(k));
+                } else if constexpr (F64) {
+                    xp[0] = (double)(x0 + PX(k));
+                    xp[1] = (double)(x1 + PY(k));
+                    xp[2] = (double)x2 + xth[k];
                 } else {
-                    xp[0] = F64 ? (double)(x0 + PX(k)) : (double)x0 + xr[3 * k];
-                    xp[1] = F64 ? (double)(x1 + PY(k)) : (double)x1 + xr[3 * k + 1];
+                    xp[0] = (double)x0 + xr[3 * k];
+                    xp[1] = (double)x1 + xr[3 * k + 1];
                     xp[2] = (double)x2 + xr[3 * k + 2];
                 }
             }
@@ -1036,6 +1068,10 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         double *xp = a.x_pred + ((size_t)b * (N + 1) + N) * 3;
         if constexpr (LTI) {
             xp[0] = (double)x0 + xsN0; xp[1] = (double)x1 + xsN1; xp[2] = (double)x2 + xsN2;
+        } else if constexpr (F64) {
+            xp[0] = (double)x0 + xrt0;
+            xp[1] = (double)x1 + xrt1;
+            xp[2] = (double)x2 + xth[N];
         } else {
             xp[0] = (double)x0 + xr[3 * N];
             xp[1] = (double)x1 + xr[3 * N + 1];
@@ -1049,7 +1085,12 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     if (a.slack_used) a.slack_used[b] = (uint8_t)used;
     a.status[b] = RMPC_OPTIMAL;
     if (a.iters) a.iters[b] = it;
-    if (a.prof) atomicMax(a.prof + 23, __builtin_amdgcn_s_memtime() - t_entry);
+    if (a.prof) {
+        const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+        atomicMax(a.prof + 23, t_end - t_entry);
+        atomicAdd(a.prof + 11, t_end - t_out0);         // output pass cycles (summed over lanes)
+        atomicAdd(a.prof + 12, 1ull);
+    }
 }
 
 }  // namespace rmpc
