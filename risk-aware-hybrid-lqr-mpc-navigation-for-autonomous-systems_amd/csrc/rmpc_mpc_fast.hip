@@ -918,15 +918,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     // fp32 pass of a refined request: a certified robot goes on, with its sets, to the fp64
     // refinement pass (a.refine), which writes the outputs
     const bool to_refine = a.refine && cert && finJ;
-    // Full fp64 lane-per-robot waves stage their u_seq / x_pred rows through LDS (below), so
-    // every lane stays to the end: the ones handed on take part in the staging rounds and
-    // store nothing
-#ifndef RMPC_OUT_STAGE
-#define RMPC_OUT_STAGE 1
-#endif
-    const bool stage_out = RMPC_OUT_STAGE && F64 && PR == 1 && (int64_t)(blockIdx.x + 1) * RMPC_WAVE <= n;
-    const bool writes = cert && finJ && !to_refine;
-    if (!writes) {
+    if (!cert || !finJ || to_refine) {
         if constexpr (PR == 2) {           // the pair's combined row flags (bit o = obstacle o)
 #pragma unroll
             for (int i = 0; i < (N + 1) / 2; i++) {
@@ -959,7 +951,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         if (to_refine) hand_on(a.refine, a.refine_count, a.refine_sets);
         else hand_on(a.retry, a.retry_count, a.retry_sets);
         if (a.prof) atomicMax(a.prof + 23, __builtin_amdgcn_s_memtime() - t_entry);   // longest lane, entry to exit
-        if (!stage_out) return;
+        return;
     }
 #pragma unroll
     for (int k = 0; k < N; k++) asm volatile("" : "+v"(S[k]), "+v"(Cs[k]), "+v"(V0[k]));
@@ -997,31 +989,6 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         if constexpr (PR == 2) gt.ld_pair(j, go[j], pp);
         else gt.ld(j, go[j]);
     }
-    // Staged rows: a per-lane store of one element writes 64 different lines of a robot-major
-    // array (64 L2 write transactions per instruction; ~52k cycles per lane for this pass at
-    // config 3 under full-chip load).  Instead each lane buffers 16 consecutive elements of its
-    // row, the wave transposes them through the setup's LDS scratch, and each 16-lane group
-    // stores 16 consecutive elements of one robot's row: 4 robots x 128 B per instruction.
-    // Robots handed on (bit clear in `wmask`) are not stored.
-    constexpr int SPO = 17;
-    double *const stgo = lds_raw + (size_t)3 * N * LW * sizeof(T) / sizeof(double);
-    const uint64_t wmask = stage_out ? (uint64_t)__builtin_amdgcn_ballot_w64(writes) : 0ull;
-    const int orr = lane >> 4, oee = lane & 15;
-    double ubuf[16], xbuf[16];
-    auto flush = [&](double *dst, const int R, const int c, const int ne, const double *buf)
-        __attribute__((always_inline)) {
-        __syncthreads();                                   // the previous round's reads are done
-#pragma unroll
-        for (int i = 0; i < 16; i++) stgo[lane * SPO + i] = buf[i];
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-            const int r = 4 * q + orr;                      // robot (lane) r of the wave
-            const int br = __shfl((int)b, r);
-            const double v = stgo[r * SPO + oee];
-            if (oee < ne && ((wmask >> r) & 1ull)) dst[(size_t)br * R + 16 * c + oee] = v;
-        }
-    };
 #pragma unroll
     for (int j = 0; j < NB; j++) {
         T du0, du1;
@@ -1065,27 +1032,6 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                 uc0 = v0;
                 uc1 = v1;
             }
-            if (stage_out) {
-                if (a.u_seq) {
-                    ubuf[(2 * k) & 15] = v0;
-                    ubuf[(2 * k + 1) & 15] = v1;
-                    if (((2 * k + 1) & 15) == 15) flush(a.u_seq, 2 * N, (2 * k + 1) >> 4, 16, ubuf);
-                }
-                if (a.x_pred) {
-                    double xv[3];
-                    if constexpr (LTI) {
-                        xv[0] = (double)(x0 + PX(k)); xv[1] = (double)(x1 + PY(k)); xv[2] = (double)(x2 + V1(k));
-                    } else {
-                        xv[0] = (double)(x0 + PX(k)); xv[1] = (double)(x1 + PY(k)); xv[2] = (double)x2 + xth[k];
-                    }
-#pragma unroll
-                    for (int cc = 0; cc < 3; cc++) {
-                        const int e = 3 * k + cc;
-                        xbuf[e & 15] = xv[cc];
-                        if ((e & 15) == 15) flush(a.x_pred, 3 * (N + 1), e >> 4, 16, xbuf);
-                    }
-                }
-            } else {
             if (a.u_seq) {
                 a.u_seq[((size_t)b * N + k) * 2] = v0;
                 a.u_seq[((size_t)b * N + k) * 2 + 1] = v1;
@@ -1104,7 +1050,6 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                     xp[2] = (double)x2 + xr[3 * k + 2];
                 }
             }
-            }
             if constexpr (LTI) {
                 const T n0 = x0 + la0 * x2 + lb0 * du0 + S[k];
                 const T n1 = x1 + la1 * x2 + lb1 * du0 + Cs[k];
@@ -1119,26 +1064,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             }
         }
     }
-    if (stage_out) {
-        // the terminal row, then the rows' last partial chunks
-        if (a.x_pred) {
-            double xv[3];
-            if constexpr (LTI) {
-                xv[0] = (double)x0 + xsN0; xv[1] = (double)x1 + xsN1; xv[2] = (double)x2 + xsN2;
-            } else {
-                xv[0] = (double)x0 + xrt0; xv[1] = (double)x1 + xrt1; xv[2] = (double)x2 + xth[N];
-            }
-#pragma unroll
-            for (int cc = 0; cc < 3; cc++) {
-                const int e = 3 * N + cc;
-                xbuf[e & 15] = xv[cc];
-                if ((e & 15) == 15) flush(a.x_pred, 3 * (N + 1), e >> 4, 16, xbuf);
-            }
-            if ((3 * (N + 1)) & 15) flush(a.x_pred, 3 * (N + 1), (3 * (N + 1)) >> 4, (3 * (N + 1)) & 15, xbuf);
-        }
-        if (a.u_seq && ((2 * N) & 15)) flush(a.u_seq, 2 * N, (2 * N) >> 4, (2 * N) & 15, ubuf);
-        if (!writes) return;
-    } else if (a.x_pred) {
+    if (a.x_pred) {
         double *xp = a.x_pred + ((size_t)b * (N + 1) + N) * 3;
         if constexpr (LTI) {
             xp[0] = (double)x0 + xsN0; xp[1] = (double)x1 + xsN1; xp[2] = (double)x2 + xsN2;
