@@ -964,13 +964,14 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     const int sc = (!LTI && a.step_count) ? a.step_count[b] : 0;
     T x0 = d0, x1 = d1, x2 = d2;
     double uc0 = 0, uc1 = 0;
-    // The gains are prefetched PFO blocks ahead, as in the forward sweep.  A block's loads are
+    // The gains are prefetched PFO blocks ahead (8: 98 AGPRs against 136 at 4 -- the allocation
+    // of the whole kernel moves -- and one batch alone 185.4M -> 188.7M solves/s at config 3).  A block's loads are
     // issued before the previous steps' output stores, and vmcnt counts loads and stores in
     // issue order, so a load-use wait never waits for those stores: loading each block at its
     // own step made every step wait for all earlier stores to complete (round 3: ~106k cycles
     // per lane for this pass at config 3 under full-chip load).
 #ifndef RMPC_PFO
-#define RMPC_PFO 4
+#define RMPC_PFO 8
 #endif
     constexpr int PFO = RMPC_PFO;
     // x_pred's reference rows (LTV: the heading as given, not unwrapped; fp32 also the
