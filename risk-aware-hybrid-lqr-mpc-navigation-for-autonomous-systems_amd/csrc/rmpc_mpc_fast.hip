@@ -441,7 +441,10 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         it = (int)ws[(N + NB) * a.B];
         if (it > 0) hist0 = set_sig();
     }
-    else if (a.init_zc) {
+#ifndef RMPC_INIT_ZC_BUILD
+#define RMPC_INIT_ZC_BUILD 1
+#endif
+    else if (RMPC_INIT_ZC_BUILD && a.init_zc) {
         // Zero-correction start: the hinge rows the reference inputs alone would violate start
         // active (the free response x_{k+1} = A_k x_k (+ c_k), du = 0).  The QP and its optimum
         // are unchanged; only the first PDAS iterate is closer to it.
