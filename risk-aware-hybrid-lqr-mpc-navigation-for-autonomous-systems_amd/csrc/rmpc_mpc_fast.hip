@@ -483,6 +483,24 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     }
     // (fp64 refinement of fp32-certified sets: `extra_cap` more PDAS solves from them)
     const int maxit = a.extra_cap > 0 ? min(p.max_iter, it + a.extra_cap) : maxit0;
+    // The last GREG blocks the backward sweep forms (j < GREG) stay in registers instead of the
+    // tile: the forward sweep and the output pass read them first, and a tile load of them
+    // waits (in-order vmcnt) for every store of the sweep to complete.  Config 3's fp64 LTV
+    // instances only (4 blocks: in flight 336.6-338.1M -> 345.0-350.7M solves/s, one batch
+    // alone 188.0M -> 191.2M); elsewhere the extra registers spill.
+#ifndef RMPC_GREG
+#define RMPC_GREG 4
+#endif
+    constexpr int GREG0 = (F64 && PR == 1 && !LTI && N == 20 && BS == 1) ? RMPC_GREG : 0;
+    constexpr int GREG = GREG0 < NB ? GREG0 : NB;
+    T greg[GREG > 0 ? GREG : 1][8];
+    auto gload = [&](const int j, T *dst) __attribute__((always_inline)) {
+        if (j < GREG) {
+#pragma unroll
+            for (int q = 0; q < 8; q++) dst[q] = greg[j < GREG ? j : 0][q];
+        } else if constexpr (PR == 2) gt.ld_pair(j, dst, pp);
+        else gt.ld(j, dst);
+    };
     while (fin && it < maxit) {
         it++;
         // Keep the per-step inputs opaque to the optimiser at every iteration: otherwise it
@@ -648,7 +666,10 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
                 const int bf0 = bfj & 3, bf1 = (bfj >> 2) & 3;
                 V = ric_block_bf(W, bf0, bf1, bf0 == 1 ? lo0 : hi0, bf1 == 1 ? lo1 : hi1, G);
             }
-            if constexpr (PR == 2) gt.st_half(j, G, pp);
+            if (j < GREG) {
+#pragma unroll
+                for (int q = 0; q < 8; q++) greg[j < GREG ? j : 0][q] = G[q];
+            } else if constexpr (PR == 2) gt.st_half(j, G, pp);
             else gt.st(j, G);
 #ifndef RMPC_BSB
 #define RMPC_BSB 0
@@ -673,8 +694,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         T g[NB][8];
 #pragma unroll
         for (int j = 0; j < NB && j < PF; j++) {
-            if constexpr (PR == 2) gt.ld_pair(j, g[j], pp);
-            else gt.ld(j, g[j]);
+            gload(j, g[j]);
         }
 #ifndef RMPC_FPF
 #define RMPC_FPF 1
@@ -696,8 +716,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
 #pragma unroll
         for (int j = 0; j < NB; j++) {
             if (j + PF < NB) {
-                if constexpr (PR == 2) gt.ld_pair(j + PF, g[j + PF], pp);
-                else gt.ld(j + PF, g[j + PF]);
+                gload(j + PF, g[j + PF]);
             }
             if constexpr (UF && BS == 1) {
                 // Compile-time rows, block size 1: the step with wave-mask (SGPR) set logic.
@@ -990,8 +1009,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     T go[NB][8];
 #pragma unroll
     for (int j = 0; j < NB && j < PFO; j++) {
-        if constexpr (PR == 2) gt.ld_pair(j, go[j], pp);
-        else gt.ld(j, go[j]);
+        gload(j, go[j]);
     }
 #pragma unroll
     for (int j = 0; j < NB; j++) {
@@ -999,8 +1017,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         const int k0 = j * BS;
         const int k1 = (k0 + BS < N) ? k0 + BS : N;
         if (j + PFO < NB) {
-            if constexpr (PR == 2) gt.ld_pair(j + PFO, go[j + PFO], pp);
-            else gt.ld(j + PFO, go[j + PFO]);
+            gload(j + PFO, go[j + PFO]);
         }
         {   // the certified inputs, re-derived from the last backward sweep's gains along the
             // same trajectory (no per-iteration input tile)
