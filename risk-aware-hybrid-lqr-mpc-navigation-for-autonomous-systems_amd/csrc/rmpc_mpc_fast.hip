@@ -936,6 +936,38 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             atomicAdd(a.prof + 56 + (mi < 7ull ? mi : 7ull), 1ull);     // waves per loop count
         }
     }
+    // The output pass's loads are issued here, before the hand-off's record stores of this
+    // wave's other lanes, for the same vmcnt reason (below); not in an fp32 pass that hands
+    // every certified robot to the refinement pass (it writes no outputs)
+    const bool may_write = !a.refine;
+    const int sc = (!LTI && a.step_count && may_write) ? a.step_count[b] : 0;
+    T x0 = d0, x1 = d1, x2 = d2;
+    double uc0 = 0, uc1 = 0;
+    // The gains are prefetched PFO blocks ahead (8: 98 AGPRs against 136 at 4 -- the allocation
+    // of the whole kernel moves -- and one batch alone 185.4M -> 188.7M solves/s at config 3).  A block's loads are
+    // issued before the previous steps' output stores, and vmcnt counts loads and stores in
+    // issue order, so a load-use wait never waits for those stores: loading each block at its
+    // own step made every step wait for all earlier stores to complete (round 3: ~106k cycles
+    // per lane for this pass at config 3 under full-chip load).
+#ifndef RMPC_PFO
+#define RMPC_PFO 8
+#endif
+    constexpr int PFO = RMPC_PFO;
+    // x_pred's reference rows (LTV: the heading as given, not unwrapped; fp32 also the
+    // positions) loaded before the first output store, for the same reason
+    double xth[(!LTI && F64) ? N + 1 : 1], xrt0 = 0, xrt1 = 0;
+    if constexpr (!LTI && F64) {
+        if (a.x_pred && may_write) {
+#pragma unroll
+            for (int k = 0; k <= N; k++) xth[k] = xr[3 * k + 2];
+            xrt0 = xr[3 * N]; xrt1 = xr[3 * N + 1];
+        }
+    }
+    T go[NB][8];
+    if (may_write) {
+#pragma unroll
+        for (int j = 0; j < NB && j < PFO; j++) gload(j, go[j]);
+    }
     const bool finJ = isfinite(J);
     // fp32 pass of a refined request: a certified robot goes on, with its sets, to the fp64
     // refinement pass (a.refine), which writes the outputs
@@ -983,34 +1015,6 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     // LTI: u = du (no u_ref), x_pred = e + x_ref (absolute), no ramp or step count.
     if (PR == 2 && pp) return;             // paired lanes: lane 2r writes the outputs
     const unsigned long long t_out0 = a.prof ? __builtin_amdgcn_s_memtime() : 0ull;   // (diagnostics)
-    const int sc = (!LTI && a.step_count) ? a.step_count[b] : 0;
-    T x0 = d0, x1 = d1, x2 = d2;
-    double uc0 = 0, uc1 = 0;
-    // The gains are prefetched PFO blocks ahead (8: 98 AGPRs against 136 at 4 -- the allocation
-    // of the whole kernel moves -- and one batch alone 185.4M -> 188.7M solves/s at config 3).  A block's loads are
-    // issued before the previous steps' output stores, and vmcnt counts loads and stores in
-    // issue order, so a load-use wait never waits for those stores: loading each block at its
-    // own step made every step wait for all earlier stores to complete (round 3: ~106k cycles
-    // per lane for this pass at config 3 under full-chip load).
-#ifndef RMPC_PFO
-#define RMPC_PFO 8
-#endif
-    constexpr int PFO = RMPC_PFO;
-    // x_pred's reference rows (LTV: the heading as given, not unwrapped; fp32 also the
-    // positions) loaded before the first output store, for the same reason
-    double xth[(!LTI && F64) ? N + 1 : 1], xrt0 = 0, xrt1 = 0;
-    if constexpr (!LTI && F64) {
-        if (a.x_pred) {
-#pragma unroll
-            for (int k = 0; k <= N; k++) xth[k] = xr[3 * k + 2];
-            xrt0 = xr[3 * N]; xrt1 = xr[3 * N + 1];
-        }
-    }
-    T go[NB][8];
-#pragma unroll
-    for (int j = 0; j < NB && j < PFO; j++) {
-        gload(j, go[j]);
-    }
 #pragma unroll
     for (int j = 0; j < NB; j++) {
         T du0, du1;
