@@ -619,12 +619,27 @@ def bench_other(args, world, rank, local, dist, pre=None):
                     f"0.767 m of an obstacle edge, {B_per} robots/GPU")
     elapsed, k_ms = _timed(args, step, dist, dev, S)
     k_avg_s = float(np.mean(k_ms)) / 1e3
+    alone_default_s = None
+    if args.config == "cfg5" and caps[0]:
+        # one batch alone with the library's default caps (what one batch at a time would use)
+        rmpc.batch.set_stage_caps(0, 0, device=local, slot=0)
+        stream0 = torch.cuda.current_stream()
+        ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps + 2)]
+        for a, b in ev2:
+            a.record(stream0)
+            step(0)
+            b.record(stream0)
+        torch.cuda.synchronize()
+        alone_default_s = float(np.mean([a.elapsed_time(b) for a, b in ev2[2:]])) / 1e3
+        rmpc.batch.set_stage_caps(*caps, device=local, slot=0)
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     line = {"metric": metric, "value": B_total * args.steps / elapsed,
             "value_one_batch_alone": B_total / k_avg_s, "unit": unit, "n_gpus": world,
+            **({"value_one_batch_alone_default_caps": B_total / alone_default_s} if alone_default_s else {}),
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: Figure-8 references at per-robot time offsets + seeded start noise",

@@ -95,6 +95,14 @@ struct RmpcCtx {
     int count_set = 0;
     bool counts_zero[2] = {false, false};
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // hybrid step: two pairs of branch counters (words 0-1 and 16-17 of `counts`), alternated
+    // per step; each step's switch kernel zeroes the pair the next step takes (hyb_ready: both
+    // pairs are in that state).  The LQR branch runs on `side`, forked from and joined back to
+    // the step's stream (hev), beside the MPC branch's half-empty lane-per-robot stage.
+    int hyb_set = 0;
+    bool hyb_ready = false;
+    hipStream_t side = nullptr;
+    hipEvent_t hev[2] = {nullptr, nullptr};
     std::mutex mu;
     // multi-device context (rmpc_ctx_create_multi): one single-device context per entry;
     // empty for a single-device context
@@ -239,6 +247,12 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     c->fast_gains.release();
     c->retry.release();
     for (auto &e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->side) {
+        (void)hipStreamSynchronize(c->side);
+        (void)hipStreamDestroy(c->side);
+    }
+    for (auto &e : c->hev)
         if (e) (void)hipEventDestroy(e);
     c->retry2.release();
     c->retry_sets.release();
@@ -990,27 +1004,43 @@ static int hybrid_step(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams
     HIP_TRY(c->idx_mpc.ensure((size_t)B * sizeof(int32_t)));
     HIP_TRY(c->counts.ensure(256));
     HIP_TRY(c->hyb_status.ensure((size_t)B * sizeof(int32_t)));
-    int32_t *cnt = (int32_t *)c->counts.p;
-    HIP_TRY(hipMemsetAsync(cnt, 0, 16, s));
+    if (!c->side) HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    for (auto &e : c->hev)
+        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    int32_t *const cbase = (int32_t *)c->counts.p;
+    if (!c->hyb_ready) {          // first step (or after a failed launch): zero both pairs
+        HIP_TRY(hipMemsetAsync(cbase, 0, 32 * sizeof(int32_t), s));
+        c->hyb_set = 0;
+    }
+    c->hyb_ready = false;
+    int32_t *const cnt = cbase + 16 * c->hyb_set;
     // pred [B][N+1][3] (rollouts with use_predicted): read here for the robots whose previous
     // step ran MPC, then overwritten by this step's MPC branch
     HIP_TRY(rmpc_launch_hybrid_decide(to_dev(rp), B, x, obstacles, n_obs, prev_ctrl, steps_since, used_mpc,
                                       risk_out, (int32_t *)c->idx_lqr.p, (int32_t *)c->idx_mpc.p, cnt, s, pred,
-                                      mp->horizon + 1));
-    // LQR branch: x_ref / u_ref = row 0 of the segment (get_reference_at_index(k))
+                                      mp->horizon + 1, cbase + 16 * (1 - c->hyb_set)));
+    c->hyb_set ^= 1;
+    c->hyb_ready = true;
+    // LQR branch on the side stream: x_ref / u_ref = row 0 of the segment
+    // (get_reference_at_index(k)).  The branches touch disjoint robots.
+    HIP_TRY(hipEventRecord(c->hev[0], s));
+    HIP_TRY(hipStreamWaitEvent(c->side, c->hev[0], 0));
     LqrDevParams ld = to_dev(lp);
     ld.ref_off = ref_off;
     HIP_TRY(rmpc_launch_lqr_control(ld, B, x, x_refs, ref_rows * 3, u_refs, uref_rows * 2, cache,
                                     u_out, nullptr, nullptr, nullptr, nullptr, (const int32_t *)c->idx_lqr.p,
-                                    cnt, s));
+                                    cnt, c->side));
+    HIP_TRY(hipEventRecord(c->hev[1], c->side));
     // MPC branch: solve_with_ltv on the segment; writes u0 straight into u_out
     // the MPC branch holds only the robots near an obstacle: about half the batch, all of
     // them in the hard part of the distribution, so the tail has room for more of them and a
     // lower fast cap pays (BASELINE config 5 sweep: cap 6 77.9M against 76.4M at cap 7)
-    return launch_mpc(c, mp, B, x, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs, step_count, u_out,
-                      nullptr, pred, nullptr, (int32_t *)c->hyb_status.p, nullptr, nullptr,
-                      (const int32_t *)c->idx_mpc.p, cnt + 1, s, ref_off,
-                      c->fast_cap > 0 ? c->fast_cap : (mp->horizon <= 20 ? 6 : 0));
+    const int rc = launch_mpc(c, mp, B, x, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs, step_count, u_out,
+                              nullptr, pred, nullptr, (int32_t *)c->hyb_status.p, nullptr, nullptr,
+                              (const int32_t *)c->idx_mpc.p, cnt + 1, s, ref_off,
+                              c->fast_cap > 0 ? c->fast_cap : (mp->horizon <= 20 ? 6 : 0));
+    HIP_TRY(hipStreamWaitEvent(s, c->hev[1], 0));    // join: the step ends when both branches have
+    return rc;
 }
 
 extern "C" int rmpc_hybrid_step_batch_dev(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams *lp,

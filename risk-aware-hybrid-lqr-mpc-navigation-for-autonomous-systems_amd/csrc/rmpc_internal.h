@@ -170,7 +170,8 @@ hipError_t rmpc_launch_hybrid_decide(const RiskDevParams &p, int64_t B, const do
                                      const double *obstacles, int n_obs, int32_t *prev_ctrl,
                                      int32_t *steps_since, uint8_t *used_mpc, double *risk_out,
                                      int32_t *idx_lqr, int32_t *idx_mpc, int32_t *counts,
-                                     hipStream_t stream, const double *pred = nullptr, int n_pred = 0);
+                                     hipStream_t stream, const double *pred = nullptr, int n_pred = 0,
+                                     int32_t *zero_next = nullptr);
 hipError_t rmpc_launch_plant(int64_t B, const double *x, const double *u, double dt, double v_max,
                              double omega_max, int method, double *x_next, hipStream_t stream);
 hipError_t rmpc_launch_figure8_table(int64_t B, const int32_t *start, int32_t k, int rows, int32_t table_len,

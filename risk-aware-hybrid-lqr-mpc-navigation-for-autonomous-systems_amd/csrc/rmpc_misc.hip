@@ -83,8 +83,11 @@ __global__ __launch_bounds__(DECIDE_BLK) void hybrid_decide_kernel(RiskDevParams
                                                                    int32_t *steps_since, uint8_t *used_mpc,
                                                                    double *risk_out, int32_t *idx_lqr,
                                                                    int32_t *idx_mpc, int32_t *counts,
-                                                                   const double *pred, int n_pred) {
+                                                                   const double *pred, int n_pred, int32_t *zero_next) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // the other counter pair, which the previous step used (complete in stream order) and the
+    // next step takes: zeroed here instead of a fill launch per step
+    if (zero_next && b < 2) zero_next[b] = 0;
     const bool valid = b < B;
     bool mpc = false;
     if (valid) {
@@ -315,10 +318,11 @@ hipError_t rmpc_launch_hybrid_decide(const RiskDevParams &p, int64_t B, const do
                                      const double *obstacles, int n_obs, int32_t *prev_ctrl,
                                      int32_t *steps_since, uint8_t *used_mpc, double *risk_out,
                                      int32_t *idx_lqr, int32_t *idx_mpc, int32_t *counts,
-                                     hipStream_t stream, const double *pred, int n_pred) {
+                                     hipStream_t stream, const double *pred, int n_pred, int32_t *zero_next) {
     if (B <= 0) return hipSuccess;
     hipLaunchKernelGGL(hybrid_decide_kernel, dim3(nblk(B, DECIDE_BLK)), dim3(DECIDE_BLK), 0, stream, p, B, x, obstacles,
-                       n_obs, prev_ctrl, steps_since, used_mpc, risk_out, idx_lqr, idx_mpc, counts, pred, n_pred);
+                       n_obs, prev_ctrl, steps_since, used_mpc, risk_out, idx_lqr, idx_mpc, counts, pred, n_pred,
+                       zero_next);
     return hipGetLastError();
 }
 

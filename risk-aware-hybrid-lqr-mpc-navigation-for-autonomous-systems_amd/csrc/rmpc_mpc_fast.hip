@@ -494,10 +494,26 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     constexpr int GREG0 = (F64 && PR == 1 && !LTI && N == 20 && BS == 1) ? RMPC_GREG : 0;
     constexpr int GREG = GREG0 < NB ? GREG0 : NB;
     T greg[GREG > 0 ? GREG : 1][8];
+    // The next GLDS blocks (GREG <= j < GREG + GLDS) go to the setup's staging scratch in LDS,
+    // free once the setup is done: [block][pair q][lane] pairs, each lane its own slots (a wave
+    // per workgroup, so no barrier).  LDS accesses count in lgkmcnt, not behind the tile stores.
+#ifndef RMPC_GLDS
+#define RMPC_GLDS 2
+#endif
+    constexpr int GLDS = (GREG > 0 && GREG + RMPC_GLDS <= NB) ? RMPC_GLDS : 0;
+    static_assert(GLDS * 8 * RMPC_WAVE * sizeof(T) <= RMPC_WAVE * 17 * sizeof(double), "LDS gain blocks exceed the scratch");
+    struct alignas(2 * sizeof(T)) GPair { T x, y; };
+    GPair *const glds = reinterpret_cast<GPair *>(lds_raw + (size_t)3 * N * LW * sizeof(T) / sizeof(double)) + lane;
     auto gload = [&](const int j, T *dst) __attribute__((always_inline)) {
         if (j < GREG) {
 #pragma unroll
             for (int q = 0; q < 8; q++) dst[q] = greg[j < GREG ? j : 0][q];
+        } else if (j < GREG + GLDS) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const GPair v = glds[((j - GREG) * 4 + q) * RMPC_WAVE];
+                dst[2 * q] = v.x; dst[2 * q + 1] = v.y;
+            }
         } else if constexpr (PR == 2) gt.ld_pair(j, dst, pp);
         else gt.ld(j, dst);
     };
@@ -669,6 +685,9 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
             if (j < GREG) {
 #pragma unroll
                 for (int q = 0; q < 8; q++) greg[j < GREG ? j : 0][q] = G[q];
+            } else if (j < GREG + GLDS) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) glds[((j - GREG) * 4 + q) * RMPC_WAVE] = GPair{G[2 * q], G[2 * q + 1]};
             } else if constexpr (PR == 2) gt.st_half(j, G, pp);
             else gt.st(j, G);
 #ifndef RMPC_BSB
