@@ -103,6 +103,10 @@ struct RmpcCtx {
     bool hyb_ready = false;
     hipStream_t side = nullptr;
     hipEvent_t hev[2] = {nullptr, nullptr};
+    // fp32 requests: the fp64 refinement pass runs on `side` beside the tail (rev: fork/join);
+    // the robots it hands on go to a list of their own (retry_r, sets retry_sets_r)
+    hipEvent_t rev[2] = {nullptr, nullptr};
+    DevBuf retry_r, retry_sets_r;
     std::mutex mu;
     // multi-device context (rmpc_ctx_create_multi): one single-device context per entry;
     // empty for a single-device context
@@ -254,6 +258,10 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     }
     for (auto &e : c->hev)
         if (e) (void)hipEventDestroy(e);
+    for (auto &e : c->rev)
+        if (e) (void)hipEventDestroy(e);
+    c->retry_r.release();
+    c->retry_sets_r.release();
     c->retry2.release();
     c->retry_sets.release();
     c->retry_a.release();
@@ -591,6 +599,18 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             }
         }
         HIP_TRY(rmpc_launch_mpc_fast(a, p->horizon, bs, p->precision, s, lti));
+        // tail: the lane-group Riccati kernel (default) or the condensed wave-per-robot one
+        // (RMPC_TAIL=dense); RMPC_DISABLE_DENSE skips the tail stage altogether
+        const char *tail = rmpc_knob("RMPC_TAIL");
+        const bool use_dense = tail && !strcmp(tail, "dense") && !lti &&   // the dense tail is LTV-only
+                               rmpc_mpc_dense_supported(p->horizon, bs, n_obs);   // (and built: make DENSE=1)
+        const bool group_tail = !use_dense && rmpc_mpc_group_supported(p->horizon, bs, n_obs) &&
+                                !rmpc_knob("RMPC_DISABLE_DENSE");
+        // The refinement and the tail work on disjoint robots (the fp32 pass's certified ones
+        // and the rest): the refinement runs on the side stream while the tail runs here, and
+        // the robots it hands on get a second, short tail launch after the join
+        // (RMPC_REFINE_INLINE=1: refinement, then one tail, on this stream; A/B)
+        const bool refine_side = refine && group_tail && !rmpc_knob("RMPC_REFINE_INLINE");
         if (refine) {
             dbg_sync(s, "fast (fp32 sets)");
             MpcFastArgs r = a;
@@ -603,30 +623,48 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             // whose slowest waves set the pass's length)
             r.extra_cap = rmpc_knob("RMPC_REFINE_CAP") ? atoi(rmpc_knob("RMPC_REFINE_CAP")) : 1;
             r.prof = pc ? pc + 64 : nullptr;   // (diagnostics: the refinement pass's own counters)
-            HIP_TRY(rmpc_launch_mpc_fast(r, p->horizon, bs, RMPC_F64, s, lti));
+            hipStream_t rs = s;
+            if (refine_side) {
+                if (!c->side) HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+                for (auto &e : c->rev)
+                    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                HIP_TRY(c->retry_r.ensure((size_t)B * sizeof(int32_t)));
+                HIP_TRY(c->retry_sets_r.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
+                r.retry = (int32_t *)c->retry_r.p;
+                r.retry_count = cnt + 10;
+                r.retry_sets = (uint32_t *)c->retry_sets_r.p;
+                HIP_TRY(hipEventRecord(c->rev[0], s));
+                HIP_TRY(hipStreamWaitEvent(c->side, c->rev[0], 0));
+                rs = c->side;
+            }
+            HIP_TRY(rmpc_launch_mpc_fast(r, p->horizon, bs, RMPC_F64, rs, lti));
+            if (refine_side) HIP_TRY(hipEventRecord(c->rev[1], c->side));
         }
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[1], s));
         dbg_sync(s, "fast");
         const int32_t *left = (const int32_t *)c->retry.p;
         const int32_t *left_n = cnt;
-        // tail: the lane-group Riccati kernel (default) or the condensed wave-per-robot one
-        // (RMPC_TAIL=dense); RMPC_DISABLE_DENSE skips the tail stage altogether
-        const char *tail = rmpc_knob("RMPC_TAIL");
-        const bool use_dense = tail && !strcmp(tail, "dense") && !lti &&   // the dense tail is LTV-only
-                               rmpc_mpc_dense_supported(p->horizon, bs, n_obs);   // (and built: make DENSE=1)
         // tail PDAS cap before projected Newton (sweeps: 4 at N <= 20, 6 beyond -- config 4)
         const int tail_cap = rmpc_knob("RMPC_DENSE_CAP") ? atoi(rmpc_knob("RMPC_DENSE_CAP"))
                              : c->tail_cap > 0          ? c->tail_cap
                                                         : (p->horizon <= 20 ? 4 : 6);
         // fp32 requests get the fp32 lane-group tail (RMPC_TAIL64=1: the fp64 one)
         const bool tail32 = f32 && !rmpc_knob("RMPC_TAIL64") && rmpc_mpc_group_supported(p->horizon, bs, n_obs, true);
-        if (!use_dense && rmpc_mpc_group_supported(p->horizon, bs, n_obs) && !rmpc_knob("RMPC_DISABLE_DENSE")) {
+        if (group_tail) {
             HIP_TRY(c->retry2.ensure((size_t)B * sizeof(int32_t)));
             int32_t *cnt2 = cnt + 8;
             HIP_TRY(rmpc_launch_mpc_group(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs, uref_rows,
                                           obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
                                           iters, left, left_n, (int32_t *)c->retry2.p, cnt2, tail_cap,
                                           a.retry_sets, s, pc, tail32, lti, &c->gdiag));
+            if (refine_side) {            // join, then the refinement's hand-ons (same output list)
+                HIP_TRY(hipStreamWaitEvent(s, c->rev[1], 0));
+                HIP_TRY(rmpc_launch_mpc_group(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs, uref_rows,
+                                              obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
+                                              iters, (const int32_t *)c->retry_r.p, cnt + 10, (int32_t *)c->retry2.p,
+                                              cnt2, tail_cap, (const uint32_t *)c->retry_sets_r.p, s, pc, tail32, lti,
+                                              &c->gdiag));
+            }
             if (prof) {
                 unsigned long long h[64];
                 int32_t cn[16];
@@ -635,9 +673,9 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                 HIP_TRY(hipStreamSynchronize(s));
                 const double r = h[10] ? (double)h[10] : 1.0, li = h[9] ? (double)h[9] : 1.0;
                 fprintf(stderr,
-                        "[group] in=%d out=%d rounds=%llu loop-its/round %.2f | cycles/round: setup %.0f pn-pre %.0f "
+                        "[group] in=%d (+%d from the refinement) out=%d rounds=%llu loop-its/round %.2f | cycles/round: setup %.0f pn-pre %.0f "
                         "out %.0f upd %.0f ls %.0f | per loop-it: weights %.0f back %.0f fwd %.0f rows %.0f\n",
-                        cn[0], cn[8], h[10], h[9] / r, h[0] / r, h[1] / r, h[6] / r, h[7] / r, h[8] / r,
+                        cn[0], cn[10], cn[8], h[10], h[9] / r, h[0] / r, h[1] / r, h[6] / r, h[7] / r, h[8] / r,
                         h[2] / li, h[3] / li, h[4] / li, h[5] / li);
                 fprintf(stderr, "[group] tail iterations per robot:");
                 for (int q = 0; q < 32; q++) fprintf(stderr, " %llu", h[24 + q]);

@@ -22,6 +22,6 @@ print('[$args | $v] value %.4e alone %.4e ms/step %.4f'%(d['value'],d.get('value
   if [ -n "$PROF" ]; then
     env $v RMPC_DENSE_PROF=1 timeout -k 10 200 python bench.py $args --inflight 1 --steps 2 --warmup 1 --no-cpu-baseline \
         --no-pcie > /dev/null 2> gpurun_out/ab_${tag}_prof.err || exit 1
-    grep "\[group\]\|\[fast\]\|\[dense\]\|\[refine\]" gpurun_out/ab_${tag}_prof.err | tail -4
+    grep "\[group\]\|\[fast\]\|\[dense\]\|\[refine\]" gpurun_out/ab_${tag}_prof.err | tail -5
   fi
 done
