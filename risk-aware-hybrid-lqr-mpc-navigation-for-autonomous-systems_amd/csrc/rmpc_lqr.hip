@@ -62,11 +62,96 @@ __device__ __forceinline__ bool jury3_stable(const double M[3][3]) {
            (1.0 - a0 * a0 - fabs(a1 - a0 * a2) > eps);
 }
 
+// Equal position weights (Q[0] == Q[1]: the reference's defaults [10,10,1] and config 2's
+// [15,15,8]) make the DARE rotation-invariant.  In path coordinates z = T'e, T = diag(R(theta), 1),
+// the linearisation is A~ = [[1,0,0],[0,1,v dt],[0,0,1]], B~ = [[dt,0],[0,0],[0,dt]] and Q~ = Q:
+// the speed channel is a scalar DARE with a closed-form root, the lateral/heading channel a
+// 2x2 DARE (SDA on 2x2 blocks, a third of the 3x3 flops).  P = T P~ T', K = K~ T'.
+__device__ bool lqr_gain_rotated(const LqrDevParams &p, double v_r, double s, double c, double K[6], M3 *Pout) {
+    const double dt = p.dt, q0 = p.Q[0], r0 = p.R[0], r1 = p.R[1];
+    // speed channel: p0 = q + p0 - p0^2 dt^2 / (r + p0 dt^2)  ->  p0 = q/2 + sqrt(q^2/4 + q r / dt^2)
+    const double p0 = 0.5 * q0 + sqrt(0.25 * q0 * q0 + q0 * r0 / (dt * dt));
+    const double k0 = p0 * dt / (r0 + p0 * dt * dt);
+    // lateral offset / heading: A2 = [[1, a], [0, 1]], B2 = (0, dt)', Q2 = diag(Q[1], Q[2])
+    const double a = v_r * dt;
+    double A00 = 1, A01 = a, A10 = 0, A11 = 1;
+    double G00 = 0, G01 = 0, G11 = dt * dt / r1;
+    double H00 = p.Q[1], H01 = 0, H11 = p.Q[2];
+    bool conv = false, last = false;
+    for (int it = 0; it < p.max_iter; it++) {
+        // W = I + G H, Wi = W^-1
+        const double W00 = 1 + G00 * H00 + G01 * H01, W01 = G00 * H01 + G01 * H11;
+        const double W10 = G01 * H00 + G11 * H01, W11 = 1 + G01 * H01 + G11 * H11;
+        const double det = W00 * W11 - W01 * W10;
+        if (!(fabs(det) > 0.0) || !isfinite(det)) return false;
+        const double id = 1.0 / det;
+        const double I00 = W11 * id, I01 = -W01 * id, I10 = -W10 * id, I11 = W00 * id;
+        // WiA = Wi A, WiG = Wi G
+        const double X00 = I00 * A00 + I01 * A10, X01 = I00 * A01 + I01 * A11;
+        const double X10 = I10 * A00 + I11 * A10, X11 = I10 * A01 + I11 * A11;
+        const double Y00 = I00 * G00 + I01 * G01, Y01 = I00 * G01 + I01 * G11;
+        const double Y10 = I10 * G00 + I11 * G01, Y11 = I10 * G01 + I11 * G11;
+        // A_{k+1} = A WiA; G_{k+1} = G + A WiG A'; H_{k+1} = H + A' H WiA
+        const double nA00 = A00 * X00 + A01 * X10, nA01 = A00 * X01 + A01 * X11;
+        const double nA10 = A10 * X00 + A11 * X10, nA11 = A10 * X01 + A11 * X11;
+        const double Z00 = A00 * Y00 + A01 * Y10, Z01 = A00 * Y01 + A01 * Y11;   // A WiG
+        const double Z10 = A10 * Y00 + A11 * Y10, Z11 = A10 * Y01 + A11 * Y11;
+        const double U00 = H00 * X00 + H01 * X10, U01 = H00 * X01 + H01 * X11;   // H WiA
+        const double U10 = H01 * X00 + H11 * X10, U11 = H01 * X01 + H11 * X11;
+        const double g00 = G00 + Z00 * A00 + Z01 * A01, g01 = G01 + Z00 * A10 + Z01 * A11;
+        const double g10 = G01 + Z10 * A00 + Z11 * A01, g11 = G11 + Z10 * A10 + Z11 * A11;
+        const double h00 = H00 + A00 * U00 + A10 * U10, h01 = H01 + A00 * U01 + A10 * U11;
+        const double h10 = H01 + A01 * U00 + A11 * U10, h11 = H11 + A01 * U01 + A11 * U11;
+        const double nh01 = 0.5 * (h01 + h10);
+        const double dH = fmax(fmax(fabs(h00 - H00), fabs(nh01 - H01)), fabs(h11 - H11));
+        const double nrm = fmax(fmax(fabs(h00), fabs(nh01)), fabs(h11));
+        A00 = nA00; A01 = nA01; A10 = nA10; A11 = nA11;
+        G00 = g00; G01 = 0.5 * (g01 + g10); G11 = g11;
+        H00 = h00; H01 = nh01; H11 = h11;
+        if (!isfinite(nrm)) return false;
+        if (last) { conv = true; break; }
+        if (dH <= 1e-10 * nrm) last = true;      // (as the 3x3 SDA below)
+    }
+    if (!conv) return false;
+    // K2 = (r1 + B2'P2B2)^-1 B2'P2A2
+    const double den = r1 + dt * dt * H11;
+    const double k1 = dt * H01 / den, k2 = dt * (a * H01 + H11) / den;
+    // back to the error coordinates: u = -K~ T'e
+    K[0] = k0 * c; K[1] = k0 * s; K[2] = 0;
+    K[3] = -k1 * s; K[4] = k1 * c; K[5] = k2;
+    if (Pout) {
+        const double d = p0 - H00;
+        Pout->m[0][0] = c * c * p0 + s * s * H00;
+        Pout->m[0][1] = Pout->m[1][0] = c * s * d;
+        Pout->m[1][1] = s * s * p0 + c * c * H00;
+        Pout->m[0][2] = Pout->m[2][0] = -s * H01;
+        Pout->m[1][2] = Pout->m[2][1] = c * H01;
+        Pout->m[2][2] = H11;
+    }
+    return isfinite(K[0] + K[1] + K[3] + K[4] + K[5]);
+}
+
 // DARE + gain at one operating point; returns false when the DARE fails (fallback K).
 __device__ bool lqr_gain(const LqrDevParams &p, double v_r, double th, double K[6], M3 *Pout) {
     double s, c;
     sincos(th, &s, &c);
     const double dt = p.dt;
+#ifndef RMPC_LQR_ROTATED
+#define RMPC_LQR_ROTATED 1
+#endif
+    if (RMPC_LQR_ROTATED && p.Q[0] == p.Q[1]) {
+        if (!lqr_gain_rotated(p, v_r, s, c, K, Pout)) return false;
+        // the same strict-stability test of A - BK as the general path (below)
+        const double B[3][2] = {{c * dt, 0}, {s * dt, 0}, {0, dt}};
+        const double A2[3] = {-v_r * s * dt, v_r * c * dt, 1};
+        double Mc[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++)
+                Mc[i][j] = (j == 2 ? A2[i] : (i == j ? 1.0 : 0.0)) - B[i][0] * K[j] - B[i][1] * K[3 + j];
+        return jury3_stable(Mc);
+    }
     M3 A = {{{1, 0, -v_r * s * dt}, {0, 1, v_r * c * dt}, {0, 0, 1}}};
     const double B[3][2] = {{c * dt, 0}, {s * dt, 0}, {0, dt}};
     M3 G, H = {{{p.Q[0], 0, 0}, {0, p.Q[1], 0}, {0, 0, p.Q[2]}}};
@@ -159,7 +244,12 @@ __device__ bool lqr_gain(const LqrDevParams &p, double v_r, double th, double K[
     return jury3_stable(Mc);
 }
 
-__global__ __launch_bounds__(256) void lqr_control_kernel(LqrDevParams p, int64_t B, const double *x,
+// Workgroup size: one wave (RMPC_LQR_BLK=64), so a small batch (config 2: 4096 robots, 64
+// waves) spreads over 64 CUs instead of sharing 16
+#ifndef RMPC_LQR_BLK
+#define RMPC_LQR_BLK 64
+#endif
+__global__ __launch_bounds__(RMPC_LQR_BLK) void lqr_control_kernel(LqrDevParams p, int64_t B, const double *x,
                                                           const double *x_ref, int xref_stride,
                                                           const double *u_ref, int uref_stride,
                                                           RmpcLqrCache *cache, double *u_out,
@@ -254,7 +344,7 @@ hipError_t rmpc_launch_lqr_control(const LqrDevParams &p, int64_t B, const doubl
                                    double *err_out, double *K_out, double *P_out, int32_t *status,
                                    const int32_t *index, const int32_t *count, hipStream_t stream) {
     if (B <= 0) return hipSuccess;
-    const int threads = 256;
+    const int threads = RMPC_LQR_BLK;
     hipLaunchKernelGGL(lqr_control_kernel, dim3((unsigned)((B + threads - 1) / threads)), dim3(threads), 0,
                        stream, p, B, x, x_ref, xref_stride, u_ref, uref_stride, cache, u_out, err_out,
                        K_out, P_out, status, index, count);
