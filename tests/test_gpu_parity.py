@@ -40,6 +40,26 @@ def test_lqr_gain_grid_matches_reference(rm, golden):
                            np.diag(d[f"Q_{tag}"]), np.diag(d["R"]))
 
 
+@pytest.mark.parametrize("Qd", [[12.0, 7.0, 3.0], [15.0, 15.0, 8.0], [4.0, 4.0, 0.5]])
+def test_lqr_both_dare_paths_match_scipy(rm, golden, Qd):
+    """The kernel solves the DARE in path coordinates when Q[0] == Q[1] (scalar + 2x2 SDA)
+    and with the 3x3 SDA otherwise: both against SciPy's solve_discrete_are (the reference's
+    arithmetic, lqr_controller.py:126-132, via oracle/lqr.py) on the golden (v_r, theta_r) grid,
+    conditioning-aware tolerances and DARE residuals (tests/lqr_checks.py).  Parity unpinned
+    by reference artefacts for Q = [12, 7, 3] and [4, 4, 0.5] (no reference run uses them)."""
+    d = golden("lqr.npz")
+    Q, R = np.diag(Qd), np.diag(d["R"])
+    p = rm._native.lqr_params(Qd, d["R"], 0.02, 2.0, 3.0)
+    K, P, st = rm.batch.lqr_gain_batch(p, d["grid"][:, 0], d["grid"][:, 1], guard=True)
+    Kr, Pr = np.empty_like(K), np.empty_like(P)
+    for i, (v, t) in enumerate(d["grid"]):
+        k, pp, ok = olqr.dare_gain(v, t, Q, R, 0.02)
+        assert ok
+        Kr[i], Pr[i] = k, pp
+    assert np.all(st == 0)
+    assert_gains_match(d["grid"], K, P, Kr, Pr, Q, R)
+
+
 def test_lqr_control_matches_reference(rm, golden):
     d = golden("lqr.npz")
     c = rm.LQRController([15.0, 15.0, 8.0], [0.1, 0.1], 0.02, 2.0, 3.0)
