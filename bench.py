@@ -101,6 +101,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline work budget")
     ap.add_argument("--stage-caps", default=None,
                     help="FAST,TAIL: the in-flight contexts' stage caps instead of the tuned ones (sweeps)")
+    ap.add_argument("--presort", type=int, default=0,
+                    help="A/B: order each fleet's robots by predicted difficulty within blocks of this size")
     ap.add_argument("--inflight", type=int, default=3,
                     help="MPC configs: batches in flight at once, each on its own stream with its own "
                          "solver context and outputs (step k runs on stream k mod S)")
@@ -145,6 +147,9 @@ def main():
     for f in range(S):
         xr_f, ur_f = rmpc.batch.figure8_batch(W.fleet_t0(idx, B_total, f, S), N + 1, device=local)
         x0_f = xr_f[:, 0] + W.noise_at(idx, W.fleet_seed(seed, f))
+        if args.presort:
+            o = W.block_sorted_order(W.difficulty_key(x0_f, xr_f, ur_f, obs_list), args.presort)
+            xr_f, ur_f, x0_f = xr_f[o], ur_f[o], x0_f[o]
         fleets.append(dict(x0_h=x0_f, xr_h=xr_f, ur_h=ur_f, x0=torch.from_numpy(x0_f).to(dev),
                            xr=torch.from_numpy(xr_f).to(dev), ur=torch.from_numpy(ur_f).to(dev)))
     x0_h, xr_h, ur_h = fleets[0]["x0_h"], fleets[0]["xr_h"], fleets[0]["ur_h"]
@@ -384,7 +389,7 @@ def main():
         cpu.mpc_solve_batch(cp, x0_h[sl], xr_h[sl], ur_h[sl], obs_list, step_count=sc.copy(),
                             threads=threads)   # warm
         reps, t_cpu, res = 0, 0.0, None
-        while t_cpu < args.cpu_seconds * 0.8 and reps < 50:
+        while t_cpu < args.cpu_seconds * 0.8 and reps < 1000:
             t = time.perf_counter()
             res = cpu.mpc_solve_batch(cp, x0_h[sl], xr_h[sl], ur_h[sl], obs_list,
                                       step_count=sc.copy(), threads=threads)
@@ -689,7 +694,7 @@ def bench_other(args, world, rank, local, dist, pre=None):
             xr0, ur0 = np.ascontiguousarray(xr_h[:, 0]), np.ascontiguousarray(ur_h[:, 0])
             cpu.lqr_control_batch(lq, x_h, xr0, ur0, threads=threads)
             reps, t_c = 0, 0.0
-            while t_c < args.cpu_seconds * 0.5 and reps < 200:
+            while t_c < args.cpu_seconds * 0.5 and reps < 4000:
                 t = time.perf_counter()
                 cpu.lqr_control_batch(lq, x_h, xr0, ur0, threads=threads)
                 t_c += time.perf_counter() - t
@@ -719,7 +724,7 @@ def bench_other(args, world, rank, local, dist, pre=None):
             cpu.set_pdas_caps(6, 4)        # the switch's MPC branch: fast cap 6, 4 tail solves
             cpu_step()
             reps, t_c = 0, 0.0
-            while t_c < args.cpu_seconds * 0.8 and reps < 50:
+            while t_c < args.cpu_seconds * 0.8 and reps < 1000:
                 t = time.perf_counter()
                 cpu_step()
                 t_c += time.perf_counter() - t

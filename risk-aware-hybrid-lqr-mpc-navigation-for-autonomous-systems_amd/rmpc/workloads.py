@@ -139,3 +139,33 @@ def aggregate(dist, elapsed, counts, device="cpu"):
     cc = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=device)
     dist.all_reduce(cc)
     return float(tt.item()), [int(v) for v in cc.tolist()]
+
+
+def difficulty_key(x0, xr, ur, obs, d_safe=0.3, dt=0.02):
+    """Predicted PDAS iterations of each robot (a heuristic for grouping robots into waves):
+    hinge rows the zero-correction rollout violates (the free response of the start error
+    under the reference inputs) + 8 |heading error| + 2 |position error|."""
+    x0, xr, ur = np.asarray(x0), np.asarray(xr), np.asarray(ur)
+    N = ur.shape[1] if ur.shape[1] < xr.shape[1] else xr.shape[1] - 1
+    px, py = xr[:, :N, 0], xr[:, :N, 1]
+    th = np.unwrap(xr[:, :N, 2], axis=1)
+    vr = np.where(np.abs(ur[:, :N, 0]) > 0.01, ur[:, :N, 0], 0.1)
+    e = x0 - xr[:, 0]
+    eth = np.abs((e[:, 2] + np.pi) % (2 * np.pi) - np.pi)
+    e0, e1, e2 = e[:, 0].copy(), e[:, 1].copy(), (e[:, 2] + np.pi) % (2 * np.pi) - np.pi
+    viol = np.zeros(len(x0))
+    for k in range(N):
+        if k > 0:
+            for ox, oy, r in obs:
+                dx, dy = px[:, k] - ox, py[:, k] - oy
+                dist = np.maximum(np.hypot(dx, dy), 1e-12)
+                viol += (d_safe + r - (dx * (px[:, k] + e0 - ox) + dy * (py[:, k] + e1 - oy)) / dist) > 0
+        e0 = e0 - vr[:, k] * np.sin(th[:, k]) * dt * e2
+        e1 = e1 + vr[:, k] * np.cos(th[:, k]) * dt * e2
+    return viol + 8 * eth + 2 * np.hypot(e[:, 0], e[:, 1])
+
+
+def block_sorted_order(key, blk=512):
+    """Permutation that sorts each block of `blk` consecutive robots by key (ascending)."""
+    B = len(key)
+    return np.concatenate([s + np.argsort(key[s:s + blk], kind="stable") for s in range(0, B, blk)])
