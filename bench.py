@@ -103,6 +103,8 @@ def main():
                     help="FAST,TAIL: the in-flight contexts' stage caps instead of the tuned ones (sweeps)")
     ap.add_argument("--presort", type=int, default=0,
                     help="A/B: order each fleet's robots by predicted difficulty within blocks of this size")
+    ap.add_argument("--inflight-side", action="store_true",
+                    help="keep the library's side streams on the in-flight contexts (A/B; default off there)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="MPC configs: batches in flight at once, each on its own stream with its own "
                          "solver context and outputs (step k runs on stream k mod S)")
@@ -175,6 +177,7 @@ def main():
     p = rmpc._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
                                 0.02, block_size=1, ltv=not args.lti, precision=1 if f32 else 0)
     stream = torch.cuda.current_stream()
+    alone_default_s = None
     streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(S - 1)]
     # with batches in flight the chip's idle time is filled by the other batches, and a longer
     # lane-per-robot stage (less work for the lane-group tail) pays (scripts/r02_s3_caps*.sh,
@@ -187,6 +190,10 @@ def main():
         caps = tuple(int(v) for v in args.stage_caps.split(","))
     for i in range(S):
         rmpc.batch.set_stage_caps(*caps, device=local, slot=i)
+        # in flight, the other batches overlap each other, and the side streams would add to the
+        # streams sharing the hardware queues: off there (rmpc_ctx_set_side_stream; config 4
+        # 69.9M against 66.0M solves/s, profiles/r03/ab_side_streams_in_flight.txt)
+        rmpc.batch.set_side_stream(S == 1 or args.inflight_side, device=local, slot=i)
 
     def step(k=0):
         i = k % S
@@ -223,8 +230,7 @@ def main():
     k_ms = [a.elapsed_time(b) for a, b in ev]
     k_avg_s = float(np.mean(k_ms)) / 1e3
     # ... and with the library's default stage caps on a context of its own (what one batch at
-    # a time would use)
-    alone_default_s = k_avg_s
+    # a time would use; its side stream on, rmpc_ctx_set_side_stream)
     if caps[0]:
         rmpc.batch.set_stage_caps(0, 0, device=local, slot=S)
         ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -236,6 +242,8 @@ def main():
             ev2[i][1].record(stream)
         torch.cuda.synchronize()
         alone_default_s = float(np.mean([a.elapsed_time(b) for a, b in ev2[2:]])) / 1e3
+    if alone_default_s is None or not caps[0]:
+        alone_default_s = k_avg_s
 
     # per-stage device time (separate, untimed pass: events between the pipeline's kernels)
     # (only the lane-per-robot pipeline has stages; fp32 / other horizons run one kernel)
@@ -612,6 +620,8 @@ def bench_other(args, world, rank, local, dist, pre=None):
         caps = (9, 4) if S > 1 else (0, 0)
         for i in range(S):
             rmpc.batch.set_stage_caps(*caps, device=local, slot=i)
+            # (config 5 keeps its side stream in flight: 398-418M against 233M steps/s without)
+            rmpc.batch.set_side_stream(True, device=local, slot=i)
 
         def step(k=0):
             i = k % S
@@ -627,6 +637,7 @@ def bench_other(args, world, rank, local, dist, pre=None):
     alone_default_s = None
     if args.config == "cfg5" and caps[0]:
         # one batch alone with the library's default caps (what one batch at a time would use)
+        torch.cuda.synchronize()
         rmpc.batch.set_stage_caps(0, 0, device=local, slot=0)
         stream0 = torch.cuda.current_stream()
         ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))

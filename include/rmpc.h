@@ -152,6 +152,14 @@ int rmpc_ctx_set_timing(RmpcCtx *ctx, int32_t on);
  * ((9, 4) at BASELINE configs 3 and 5).  They apply to the hybrid
  * step's MPC branch too (its default first-stage cap is 6).  fast_cap, tail_cap in [0, 64]. */
 int rmpc_ctx_set_stage_caps(RmpcCtx *ctx, int32_t fast_cap, int32_t tail_cap);
+/* Side stream on this context (a performance setting; results are identical): on (default),
+ * a pipeline's independent branch -- the fp64 refinement of an fp32 request beside the tail,
+ * the hybrid step's LQR branch beside the MPC branch -- runs on a second stream of the context,
+ * forked from and joined back to the call's stream.  Off, the branches run in order on the
+ * call's stream.  With several contexts in flight on their own streams, the side streams add
+ * to the streams sharing the device's hardware queues (GPU_MAX_HW_QUEUES), and the other
+ * batches already fill the chip: the bench turns them off there. */
+int rmpc_ctx_set_side_stream(RmpcCtx *ctx, int32_t on);
 int rmpc_mpc_stage_times(RmpcCtx *ctx, double *out3);
 
 /* ---- MPC --------------------------------------------------------------------------------

@@ -89,6 +89,7 @@ struct RmpcCtx {
     bool timing = false;
     bool timed = false;
     int fast_cap = 0, tail_cap = 0;   // rmpc_ctx_set_stage_caps (0: library default)
+    bool use_side = true;             // rmpc_ctx_set_side_stream
     // retry_count: two sets of list counters (RMPC_COUNT_WORDS words at word 0 and 32), used
     // by alternate pipelines; set k is zero in stream order when counts_zero[k] (the
     // previous pipeline's lane-per-robot kernel zeroed it), so the next needs no fill launch
@@ -190,6 +191,8 @@ int rmpc_device_count(int *count) {
     return RMPC_OK;
 }
 
+static hipStream_t own(RmpcCtx *c);
+
 int rmpc_ctx_create(int device_id, RmpcCtx **out) {
     if (!out) return fail(RMPC_EINVAL, "out is NULL");
     int n = 0;
@@ -198,10 +201,14 @@ int rmpc_ctx_create(int device_id, RmpcCtx **out) {
     HIP_TRY(hipSetDevice(device_id));
     RmpcCtx *c = new RmpcCtx();
     c->device = device_id;
-    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    if (e != hipSuccess) {
+    // The context's own stream (host-pointer entry points) is made here, also for contexts
+    // used only through the _dev entry points: creating it on first use measured slower with
+    // batches in flight (config 4 68.0M against 70.1M, config 5 402M against 419M solves/s) --
+    // the streams of a process share GPU_MAX_HW_QUEUES hardware queues, and which ones share
+    // depends on the order they are made
+    if (!own(c)) {
         delete c;
-        return fail(RMPC_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+        return fail(RMPC_EHIP, "hipStreamCreate failed");
     }
     *out = c;
     return RMPC_OK;
@@ -241,7 +248,7 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
         return RMPC_OK;
     }
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->ws.release();
     for (auto &b : c->stage) b.release();
     c->idx_lqr.release();
@@ -276,7 +283,7 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     c->prof.release();
     c->retry_count.release();
     c->gdiag.release();
-    (void)hipStreamDestroy(c->stream);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return RMPC_OK;
 }
@@ -288,7 +295,7 @@ int rmpc_ctx_synchronize(RmpcCtx *c) {
         if (rc != RMPC_OK) return rc;
     }
     if (!c->sub.empty()) return RMPC_OK;
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->stream) HIP_TRY(hipStreamSynchronize(c->stream));
     return RMPC_OK;
 }
 
@@ -314,6 +321,13 @@ int rmpc_ctx_set_stage_caps(RmpcCtx *c, int32_t fast_cap, int32_t tail_cap) {
         sc->fast_cap = fast_cap;
         sc->tail_cap = tail_cap;
     }
+    return RMPC_OK;
+}
+
+int rmpc_ctx_set_side_stream(RmpcCtx *c, int32_t on) {
+    if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
+    c->use_side = on != 0;
+    for (auto &sc : c->sub) sc->use_side = on != 0;
     return RMPC_OK;
 }
 
@@ -402,6 +416,24 @@ static RiskDevParams to_dev(const RmpcRiskParams *p) {
 static hipError_t ensure_ws(RmpcCtx *c, const MpcLayout &L, int64_t B) {
     const size_t waves = (size_t)((B + RMPC_WAVE_LANES - 1) / RMPC_WAVE_LANES);
     return c->ws.ensure(waves * (size_t)L.REC * RMPC_WAVE_LANES * sizeof(double));
+}
+
+// The side stream for a pipeline's independent branch (config 4's refinement, config 5's LQR
+// branch): one per context, created on first use.  (One stream shared by all contexts of a
+// device serialised the batches in flight through its FIFO order: config 5 fell from ~400M to
+// 233M steps/s.)
+static hipError_t side_stream(RmpcCtx *c) {
+    if (c->side) return hipSuccess;
+    const hipError_t e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+    if (e != hipSuccess) c->side = nullptr;
+    return e;
+}
+
+// The context's own stream (host-pointer entry points), created on first use; NULL (the null
+// stream) if creation fails
+static hipStream_t own(RmpcCtx *c) {
+    if (!c->stream && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) c->stream = nullptr;
+    return c->stream;
 }
 
 // _dev entry points run on the caller's stream; NULL is the null (default) stream, as in
@@ -610,7 +642,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         // and the rest): the refinement runs on the side stream while the tail runs here, and
         // the robots it hands on get a second, short tail launch after the join
         // (RMPC_REFINE_INLINE=1: refinement, then one tail, on this stream; A/B)
-        const bool refine_side = refine && group_tail && !rmpc_knob("RMPC_REFINE_INLINE");
+        const bool refine_side = refine && group_tail && c->use_side && !rmpc_knob("RMPC_REFINE_INLINE");
         if (refine) {
             dbg_sync(s, "fast (fp32 sets)");
             MpcFastArgs r = a;
@@ -625,7 +657,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             r.prof = pc ? pc + 64 : nullptr;   // (diagnostics: the refinement pass's own counters)
             hipStream_t rs = s;
             if (refine_side) {
-                if (!c->side) HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+                HIP_TRY(side_stream(c));
                 for (auto &e : c->rev)
                     if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
                 HIP_TRY(c->retry_r.ensure((size_t)B * sizeof(int32_t)));
@@ -782,7 +814,7 @@ template <typename T>
 static int h2d(RmpcCtx *c, int slot, const T *src, size_t n, T **dst) {
     if (!src) { *dst = nullptr; return RMPC_OK; }
     HIP_TRY(c->stage[slot].ensure(align_up(n * sizeof(T), 256)));
-    HIP_TRY(hipMemcpyAsync(c->stage[slot].p, src, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->stage[slot].p, src, n * sizeof(T), hipMemcpyHostToDevice, own(c)));
     *dst = (T *)c->stage[slot].p;
     return RMPC_OK;
 }
@@ -798,7 +830,7 @@ static int dalloc(RmpcCtx *c, int slot, const T *host, size_t n, T **dst) {
 template <typename T>
 static int d2h(RmpcCtx *c, T *host, const T *dev, size_t n) {
     if (!host) return RMPC_OK;
-    HIP_TRY(hipMemcpyAsync(host, dev, n * sizeof(T), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(host, dev, n * sizeof(T), hipMemcpyDeviceToHost, own(c)));
     return RMPC_OK;
 }
 
@@ -871,7 +903,7 @@ extern "C" int rmpc_mpc_solve_batch(RmpcCtx *c, const RmpcMpcParams *p, int64_t 
     RC(dalloc(c, SB_SLACK, slack_used, (size_t)B, &dsl));
     RC(dalloc(c, SB_ITERS, iters, (size_t)B, &dit));
     RC(rmpc_mpc_solve_batch_dev(c, p, B, dx0, dxr, ref_rows, dur, uref_rows, dobs, n_obs, dstep, du0,
-                                duseq, dxp, dcost, dst, dsl, dit, c->stream));
+                                duseq, dxp, dcost, dst, dsl, dit, own(c)));
     RC(d2h(c, u0, du0, (size_t)B * 2));
     RC(d2h(c, u_seq, duseq, (size_t)B * N * 2));
     RC(d2h(c, x_pred, dxp, (size_t)B * (N + 1) * 3));
@@ -880,7 +912,7 @@ extern "C" int rmpc_mpc_solve_batch(RmpcCtx *c, const RmpcMpcParams *p, int64_t 
     RC(d2h(c, slack_used, dsl, (size_t)B));
     RC(d2h(c, iters, dit, (size_t)B));
     RC(d2h(c, step_count, dstep, (size_t)B));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(own(c)));
     return RMPC_OK;
 }
 
@@ -941,14 +973,14 @@ extern "C" int rmpc_lqr_control_batch(RmpcCtx *c, const RmpcLqrParams *p, int64_
     RC(dalloc(c, SB_K, K_out, (size_t)B * 6, &dK));
     RC(dalloc(c, SB_P, P_out, (size_t)B * 9, &dP));
     RC(dalloc(c, SB_STATUS, status, (size_t)B, &dst));
-    RC(rmpc_lqr_control_batch_dev(c, p, B, dx, dxr, dur, dc, du, de, dK, dP, dst, c->stream));
+    RC(rmpc_lqr_control_batch_dev(c, p, B, dx, dxr, dur, dc, du, de, dK, dP, dst, own(c)));
     RC(d2h(c, u_out, du, (size_t)B * 2));
     RC(d2h(c, err_out, de, (size_t)B * 3));
     RC(d2h(c, K_out, dK, (size_t)B * 6));
     RC(d2h(c, P_out, dP, (size_t)B * 9));
     RC(d2h(c, status, dst, (size_t)B));
     RC(d2h(c, cache, dc, (size_t)B));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(own(c)));
     return RMPC_OK;
 }
 
@@ -977,11 +1009,11 @@ extern "C" int rmpc_lqr_gain_batch(RmpcCtx *c, const RmpcLqrParams *p, int64_t B
     RC(dalloc(c, SB_K, K_out, (size_t)B * 6, &dK));
     RC(dalloc(c, SB_P, P_out, (size_t)B * 9, &dP));
     RC(dalloc(c, SB_STATUS, status, (size_t)B, &dst));
-    HIP_TRY(rmpc_launch_lqr_gain(to_dev(p), B, dv, dth, guard_v, dK, dP, dst, c->stream));
+    HIP_TRY(rmpc_launch_lqr_gain(to_dev(p), B, dv, dth, guard_v, dK, dP, dst, own(c)));
     RC(d2h(c, K_out, dK, (size_t)B * 6));
     RC(d2h(c, P_out, dP, (size_t)B * 9));
     RC(d2h(c, status, dst, (size_t)B));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(own(c)));
     return RMPC_OK;
 }
 
@@ -1012,11 +1044,11 @@ extern "C" int rmpc_risk_batch(RmpcCtx *c, const RmpcRiskParams *rp, int64_t B, 
     RC(dalloc(c, SB_U0, out, (size_t)B * 5, &dout));
     RC(dalloc(c, SB_SLACK, use_mpc, (size_t)B, &dm));
     RC(dalloc(c, SB_STATUS, level, (size_t)B, &dl));
-    HIP_TRY(rmpc_launch_risk(to_dev(rp), B, dx, dp, n_pred, dobs, n_obs, dout, dm, dl, c->stream));
+    HIP_TRY(rmpc_launch_risk(to_dev(rp), B, dx, dp, n_pred, dobs, n_obs, dout, dm, dl, own(c)));
     RC(d2h(c, out, dout, (size_t)B * 5));
     RC(d2h(c, use_mpc, dm, (size_t)B));
     RC(d2h(c, level, dl, (size_t)B));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(own(c)));
     return RMPC_OK;
 }
 
@@ -1042,7 +1074,7 @@ static int hybrid_step(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams
     HIP_TRY(c->idx_mpc.ensure((size_t)B * sizeof(int32_t)));
     HIP_TRY(c->counts.ensure(256));
     HIP_TRY(c->hyb_status.ensure((size_t)B * sizeof(int32_t)));
-    if (!c->side) HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    if (c->use_side) HIP_TRY(side_stream(c));
     for (auto &e : c->hev)
         if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     int32_t *const cbase = (int32_t *)c->counts.p;
@@ -1059,16 +1091,20 @@ static int hybrid_step(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams
                                       mp->horizon + 1, cbase + 16 * (1 - c->hyb_set)));
     c->hyb_set ^= 1;
     c->hyb_ready = true;
-    // LQR branch on the side stream: x_ref / u_ref = row 0 of the segment
-    // (get_reference_at_index(k)).  The branches touch disjoint robots.
-    HIP_TRY(hipEventRecord(c->hev[0], s));
-    HIP_TRY(hipStreamWaitEvent(c->side, c->hev[0], 0));
+    // LQR branch on the side stream (rmpc_ctx_set_side_stream; else in order on this one):
+    // x_ref / u_ref = row 0 of the segment (get_reference_at_index(k)).  The branches touch
+    // disjoint robots.
+    const bool side = c->use_side;
+    if (side) {
+        HIP_TRY(hipEventRecord(c->hev[0], s));
+        HIP_TRY(hipStreamWaitEvent(c->side, c->hev[0], 0));
+    }
     LqrDevParams ld = to_dev(lp);
     ld.ref_off = ref_off;
     HIP_TRY(rmpc_launch_lqr_control(ld, B, x, x_refs, ref_rows * 3, u_refs, uref_rows * 2, cache,
                                     u_out, nullptr, nullptr, nullptr, nullptr, (const int32_t *)c->idx_lqr.p,
-                                    cnt, c->side));
-    HIP_TRY(hipEventRecord(c->hev[1], c->side));
+                                    cnt, side ? c->side : s));
+    if (side) HIP_TRY(hipEventRecord(c->hev[1], c->side));
     // MPC branch: solve_with_ltv on the segment; writes u0 straight into u_out
     // the MPC branch holds only the robots near an obstacle: about half the batch, all of
     // them in the hard part of the distribution, so the tail has room for more of them and a
@@ -1077,7 +1113,7 @@ static int hybrid_step(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams
                               nullptr, pred, nullptr, (int32_t *)c->hyb_status.p, nullptr, nullptr,
                               (const int32_t *)c->idx_mpc.p, cnt + 1, s, ref_off,
                               c->fast_cap > 0 ? c->fast_cap : (mp->horizon <= 20 ? 6 : 0));
-    HIP_TRY(hipStreamWaitEvent(s, c->hev[1], 0));    // join: the step ends when both branches have
+    if (side) HIP_TRY(hipStreamWaitEvent(s, c->hev[1], 0));   // join: the step ends when both branches have
     return rc;
 }
 
@@ -1136,7 +1172,7 @@ extern "C" int rmpc_hybrid_step_batch(RmpcCtx *c, const RmpcRiskParams *rp, cons
     RC(dalloc(c, SB_SLACK, used_mpc, (size_t)B, &dused));
     RC(dalloc(c, SB_COST, risk_out, (size_t)B, &drisk));
     RC(rmpc_hybrid_step_batch_dev(c, rp, lp, mp, B, dx, dxr, ref_rows, dur, uref_rows, dobs, n_obs, dprev,
-                                  dsince, dstep, dc, du, dused, drisk, c->stream));
+                                  dsince, dstep, dc, du, dused, drisk, own(c)));
     RC(d2h(c, u_out, du, (size_t)B * 2));
     RC(d2h(c, used_mpc, dused, (size_t)B));
     RC(d2h(c, risk_out, drisk, (size_t)B));
@@ -1144,7 +1180,7 @@ extern "C" int rmpc_hybrid_step_batch(RmpcCtx *c, const RmpcRiskParams *rp, cons
     RC(d2h(c, steps_since, dsince, (size_t)B));
     RC(d2h(c, step_count, dstep, (size_t)B));
     RC(d2h(c, cache, dc, (size_t)B));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(own(c)));
     return RMPC_OK;
 }
 
@@ -1167,9 +1203,9 @@ extern "C" int rmpc_plant_step_batch(RmpcCtx *c, int64_t B, const double *x, con
     RC(h2d(c, SB_X0, x, (size_t)B * 3, &dx));
     RC(h2d(c, SB_UREF, u, (size_t)B * 2, &du));
     RC(dalloc(c, SB_U0, x_next, (size_t)B * 3, &dn));
-    HIP_TRY(rmpc_launch_plant(B, dx, du, dt, v_max, omega_max, method, dn, c->stream));
+    HIP_TRY(rmpc_launch_plant(B, dx, du, dt, v_max, omega_max, method, dn, own(c)));
     RC(d2h(c, x_next, dn, (size_t)B * 3));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(own(c)));
     return RMPC_OK;
 }
 
@@ -1193,10 +1229,10 @@ extern "C" int rmpc_figure8_batch(RmpcCtx *c, int64_t B, const double *t0, int32
     RC(h2d(c, SB_X0, t0, (size_t)B, &dt0));
     RC(dalloc(c, SB_XREF, x_refs, (size_t)B * rows * 3, &dxr));
     RC(dalloc(c, SB_UREF, u_refs, (size_t)B * rows * 2, &dur));
-    HIP_TRY(rmpc_launch_figure8(B, dt0, rows, A, a, dt, dxr, dur, c->stream));
+    HIP_TRY(rmpc_launch_figure8(B, dt0, rows, A, a, dt, dxr, dur, own(c)));
     RC(d2h(c, x_refs, dxr, (size_t)B * rows * 3));
     RC(d2h(c, u_refs, dur, (size_t)B * rows * 2));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(own(c)));
     return RMPC_OK;
 }
 
@@ -1347,11 +1383,11 @@ extern "C" int rmpc_rollout_batch(RmpcCtx *c, const RmpcRolloutParams *rp, const
         HIP_TRY(c->stage[SB_ITERS].ensure(64));
         dcnt = (int64_t *)c->stage[SB_ITERS].p;
     }
-    RC(rmpc_rollout_batch_dev(c, rp, lp, mp, kp, B, dstart, dx0, dobs, n_obs, dst, dct, dused, dcnt, c->stream));
+    RC(rmpc_rollout_batch_dev(c, rp, lp, mp, kp, B, dstart, dx0, dobs, n_obs, dst, dct, dused, dcnt, own(c)));
     RC(d2h(c, states, dst, (size_t)B * (K + 1) * 3));
     RC(d2h(c, controls, dct, (size_t)B * K * 2));
     RC(d2h(c, used_mpc, dused, (size_t)B * K));
     if (mpc_status) RC(d2h(c, mpc_status, dcnt, (size_t)4));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(own(c)));
     return RMPC_OK;
 }

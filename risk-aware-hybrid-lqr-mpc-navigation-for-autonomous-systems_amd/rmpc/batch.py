@@ -232,6 +232,13 @@ def set_stage_caps(fast_cap=0, tail_cap=0, device=0, slot=0):
           "rmpc_ctx_set_stage_caps")
 
 
+def set_side_stream(on=True, device=0, slot=0):
+    """Side stream of one context (rmpc_ctx_set_side_stream): the refinement of fp32 requests
+    and the hybrid step's LQR branch beside the main branch (on, the default) or in order."""
+    lib = nat.load()
+    check(lib.rmpc_ctx_set_side_stream(nat.context(device, slot), int(bool(on))), "rmpc_ctx_set_side_stream")
+
+
 def mpc_stage_times(device=0):
     """Device ms of the last MPC launch: (lane-per-robot, wave-per-robot tail, generic)."""
     lib = nat.load()
