@@ -782,3 +782,43 @@ def test_mpc_fp32_config4_accuracy(rm, capsys, monkeypatch, N, obs_kind, stage):
         print(f"\n[fp32 N={N} {stage}] status ok {both.mean():.4f}; rel |du0|: median "
               f"{np.median(rel[both]):.2e} p99 {np.percentile(rel[both], 99):.2e} max {rel[both].max():.2e}")
     assert rel[both].max() <= 1e-4          # the north star's control-error bound
+
+
+def test_side_stream_on_off_bitwise_identical(rm):
+    """rmpc_ctx_set_side_stream: the refinement of an fp32 request beside the tail and the
+    hybrid step's LQR branch beside the MPC branch (forked side stream) give bitwise the same
+    results as running the branches in order on the call's stream."""
+    from rmpc import workloads as W
+    outs = {}
+    B = 4096
+    idx = np.arange(B)
+    try:
+        for on in (True, False):
+            rm.batch.set_side_stream(on)
+            # fp32 request at config 4's shape: fp32 sets, fp64 refinement, fp64 tail
+            xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, W.t0_at(idx, B), 31)
+            x0 = xr[:, 0] + W.noise_at(idx, 2)
+            p = rm._native.mpc_params(30, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                                      0.02, block_size=1, precision=1)
+            r = rm.batch.mpc_solve_batch(p, x0, xr, ur, W.UNION8_OBS, step_count=np.full(B, 10, np.int32))
+            # hybrid step at config 5's shape, three steps from a fresh switch state
+            xr5, ur5 = figure8.offset_segments(2.0, 0.5, 0.02, W.cfg5_t0(idx), 21)
+            x5 = xr5[:, 0] + W.noise_at(idx, 3)
+            rp = rm._native.risk_params()
+            lp = rm._native.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0, use_cache=False)
+            mp = rm._native.mpc_params(20, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0,
+                                       0.02, block_size=1)
+            st = rm.batch.new_hybrid_state(B)
+            hs = [rm.batch.hybrid_step_batch(rp, lp, mp, x5, xr5, ur5, W.DEFAULT_OBS, st) for _ in range(3)]
+            outs[on] = (r, hs)
+    finally:
+        rm.batch.set_side_stream(True)
+    (r1, h1), (r0, h0) = outs[True], outs[False]
+    assert np.all(r1["status"] == 0)
+    for k in ("u0", "u_seq", "x_pred", "cost", "status", "iters"):
+        np.testing.assert_array_equal(r1[k], r0[k])
+    used = h1[0][1]
+    assert 0.2 < used.mean() < 0.8                     # both branches exercised
+    for a, b in zip(h1, h0):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
