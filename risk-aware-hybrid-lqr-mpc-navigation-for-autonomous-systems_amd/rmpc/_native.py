@@ -114,6 +114,9 @@ _ctx = {}
 def load():
     """Load librmpc.so and declare every exported prototype (no device needed)."""
     global _lib
+    lib = _lib
+    if lib is not None:              # (fast path: every batch call goes through here)
+        return lib
     with _lock:
         if _lib is None:
             if not os.path.exists(LIB_PATH):
@@ -159,6 +162,10 @@ def context(device=0, slot=0):
     `slot` > 0 gives further independent contexts of the same device: each owns its own
     solver scratch, so solves on different streams can be in flight at once (one context per
     stream; a context's calls must not overlap each other)."""
+    if type(device) is int and type(slot) is int:      # (fast path: an existing context)
+        ctx = _ctx.get(device if not slot else (device, "slot", slot))
+        if ctx is not None:
+            return ctx
     lib = load()
     key = int(device) if np.ndim(device) == 0 else tuple(int(d) for d in device)
     if isinstance(key, tuple) and len(key) == 1:
