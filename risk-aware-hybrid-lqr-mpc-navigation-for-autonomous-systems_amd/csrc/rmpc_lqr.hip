@@ -264,6 +264,8 @@ __global__ __launch_bounds__(RMPC_LQR_BLK) void lqr_control_kernel(LqrDevParams 
     const double *xr = x_ref + (p.ref_off ? (size_t)p.ref_off[b] * 3 : (size_t)xref_stride * b);
     const double *ur = u_ref + (p.ref_off ? (size_t)p.ref_off[b] * 2 : (size_t)uref_stride * b);
     const double v = ur[0], th = xr[2];
+    // every load before the first store (the cache update): one in-order vmcnt
+    const double x0 = xb[0], x1 = xb[1], x2 = xb[2], xr0 = xr[0], xr1 = xr[1], u1r = ur[1];
     double K[6];
     int st = RMPC_OPTIMAL;
     bool hit = false;
@@ -297,9 +299,9 @@ __global__ __launch_bounds__(RMPC_LQR_BLK) void lqr_control_kernel(LqrDevParams 
         }
     }
     // compute_control (:175-187)
-    const double e0 = xb[0] - xr[0], e1 = xb[1] - xr[1], e2 = wrap_pi(xb[2] - xr[2]);
-    const double u0 = ur[0] + -(K[0] * e0 + K[1] * e1 + K[2] * e2);
-    const double u1 = ur[1] + -(K[3] * e0 + K[4] * e1 + K[5] * e2);
+    const double e0 = x0 - xr0, e1 = x1 - xr1, e2 = wrap_pi(x2 - th);
+    const double u0 = v + -(K[0] * e0 + K[1] * e1 + K[2] * e2);
+    const double u1 = u1r + -(K[3] * e0 + K[4] * e1 + K[5] * e2);
     u_out[2 * b] = clampv(u0, -p.v_max, p.v_max);
     u_out[2 * b + 1] = clampv(u1, -p.omega_max, p.omega_max);
     if (err_out) {

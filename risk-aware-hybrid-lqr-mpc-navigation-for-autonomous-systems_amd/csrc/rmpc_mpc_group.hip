@@ -1462,13 +1462,40 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         refresh();
         if (done_ok) {
             const int sc = (!LTI && a.step_count) ? a.step_count[b] : 0;
-            for (int k = gl; k < N; k += G) {
+            constexpr bool F64 = sizeof(T) == 8;
+            // Every global load of the pass is issued before its first store: gfx950 counts
+            // loads and stores in one in-order vmcnt, so a load behind the u_seq / x_pred
+            // stores would wait for all of them to complete (the lane-per-robot kernel's
+            // output pass)
+            constexpr int KU = (N + G - 1) / G, KX = (N + 1 + G - 1) / G;
+            double urv[F64 ? 1 : KU][2], xrv[LTI ? 1 : KX][3];
+            if constexpr (!F64) {
+#pragma unroll
+                for (int i = 0; i < KU; i++) {
+                    const int k = gl + G * i;
+                    urv[i][0] = k < N ? ur[2 * k] : 0.0;
+                    urv[i][1] = k < N ? ur[2 * k + 1] : 0.0;
+                }
+            }
+            if constexpr (!LTI) {
+#pragma unroll
+                for (int i = 0; i < KX; i++) {
+                    const int k = gl + G * i;
+                    const bool in = a.x_pred && k <= N;
+                    xrv[i][0] = in ? xr[3 * k] : 0.0;
+                    xrv[i][1] = in ? xr[3 * k + 1] : 0.0;
+                    xrv[i][2] = in ? xr[3 * k + 2] : 0.0;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < KU; i++) {
+                const int k = gl + G * i;
+                if (k >= N) break;
                 const int j = k / BS;
                 // fp64: u = du + u_ref in the record; fp32: du + the fp64 u_ref (only the
                 // deviation carries fp32 rounding, as in the lane-per-robot kernel)
-                constexpr bool F64 = sizeof(T) == 8;
-                const double v0 = F64 ? (double)(ZF(2 * j) + STG(4, k)) : (double)ZF(2 * j) + ur[2 * k];
-                double v1 = F64 ? (double)(ZF(2 * j + 1) + STG(5, k)) : (double)ZF(2 * j + 1) + ur[2 * k + 1];
+                const double v0 = F64 ? (double)(ZF(2 * j) + STG(4, k)) : (double)ZF(2 * j) + urv[F64 ? 0 : i][0];
+                double v1 = F64 ? (double)(ZF(2 * j + 1) + STG(5, k)) : (double)ZF(2 * j + 1) + urv[F64 ? 0 : i][1];
                 if (!LTI && k == 0 && sc < p.ramp_up_steps) {              // :502-505 (LTV only)
                     const double lim = p.omega_max * ((double)(sc + 1) / (double)p.ramp_up_steps);
                     v1 = clampv(v1, -lim, lim);
@@ -1483,14 +1510,17 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
                 }
             }
             if (a.x_pred) {                                                 // :497
-                for (int k = gl; k <= N; k += G) {
+#pragma unroll
+                for (int i = 0; i < KX; i++) {
+                    const int k = gl + G * i;
+                    if (k > N) break;
                     double *xp = a.x_pred + ((size_t)b * (N + 1) + k) * 3;
                     if constexpr (LTI) {                                    // absolute states
                         xp[0] = (double)XF(k, 0); xp[1] = (double)XF(k, 1); xp[2] = (double)XF(k, 2);
                     } else {
-                        xp[0] = (double)XF(k, 0) + xr[3 * k];
-                        xp[1] = (double)XF(k, 1) + xr[3 * k + 1];
-                        xp[2] = (double)XF(k, 2) + xr[3 * k + 2];
+                        xp[0] = (double)XF(k, 0) + xrv[i][0];
+                        xp[1] = (double)XF(k, 1) + xrv[i][1];
+                        xp[2] = (double)XF(k, 2) + xrv[i][2];
                     }
                 }
             }
