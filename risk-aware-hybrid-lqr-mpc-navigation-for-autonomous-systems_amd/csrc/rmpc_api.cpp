@@ -685,12 +685,16 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         if (group_tail) {
             HIP_TRY(c->retry2.ensure((size_t)B * sizeof(int32_t)));
             int32_t *cnt2 = cnt + 8;
-            HIP_TRY(rmpc_launch_mpc_group(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs, uref_rows,
-                                          obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
-                                          iters, left, left_n, (int32_t *)c->retry2.p, cnt2, tail_cap,
-                                          a.retry_sets, s, pc, tail32, lti, &c->gdiag));
-            if (refine_side) {            // join, then the refinement's hand-ons (same output list)
-                HIP_TRY(hipStreamWaitEvent(s, c->rev[1], 0));
+            const hipError_t ea = rmpc_launch_mpc_group(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs,
+                                                        uref_rows, obstacles, step_count, u0, u_seq, x_pred, cost,
+                                                        status, slack_used, iters, left, left_n,
+                                                        (int32_t *)c->retry2.p, cnt2, tail_cap, a.retry_sets, s, pc,
+                                                        tail32, lti, &c->gdiag);
+            // join the refinement before anything else, also when the tail's launch failed (the
+            // call's stream must not complete ahead of the side branch)
+            if (refine_side) HIP_TRY(hipStreamWaitEvent(s, c->rev[1], 0));
+            HIP_TRY(ea);
+            if (refine_side) {            // the refinement's hand-ons (same output list)
                 HIP_TRY(rmpc_launch_mpc_group(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs, uref_rows,
                                               obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
                                               iters, (const int32_t *)c->retry_r.p, cnt + 10, (int32_t *)c->retry2.p,
