@@ -98,6 +98,7 @@ def main():
     ap.add_argument("--lti", action="store_true",
                     help="MPCController.solve (absolute-state LTI, mpc_node's path) instead of solve_with_ltv")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-closed-loop", action="store_true", help="skip the closed-loop (cold / warm) rates")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline work budget")
     ap.add_argument("--stage-caps", default=None,
                     help="FAST,TAIL: the in-flight contexts' stage caps instead of the tuned ones (sweeps)")
@@ -382,6 +383,11 @@ def main():
                       "full_outputs also returns u_seq and x_pred")
         line["pcie_inclusive"] = pc
 
+    # ---- closed loop (rank 0, N=1, config 3 only; never `value`): run_simulation.py's MPC loop
+    # on the device, cold and with the warm start across calls (rmpc_ctx_set_warm_start)
+    if world == 1 and rank == 0 and args.config == "cfg3" and not args.lti and not f32 and not args.no_closed_loop:
+        line["closed_loop"] = closed_loop(dev, B, obs_list)
+
     # ---- CPU baseline (rank 0, N=1 only): the oracle's C restatement of the same algorithm
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         from oracle import cpu
@@ -463,6 +469,77 @@ def main():
         dist.destroy_process_group()
 
 
+
+
+def closed_loop(dev, B, obs_list, K=50, fleets_max=3):
+    """run_simulation.py's MPC loop (mpc_rate 1: one solve_with_ltv per robot and control step,
+    then the plant) for fleets of B robots on the device (rmpc_rollout_batch_dev), from seeded
+    noisy starts over one Figure-8 period; 1 and `fleets_max` fleets at once (one context and
+    stream each), each from a cold start and with the warm start across calls (the reference's
+    warm_start=True / get_warm_start, mpc_controller.py:272-277, 524-538).  Median of 3 runs of
+    K steps after one untimed run.  Returns solves/s and the warm/cold closed-loop difference."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    import rmpc
+    from rmpc import _native as nat
+    from rmpc import workloads as W
+    lib = nat.load()
+    mp = nat.mpc_params(20, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+    idx = np.arange(B)
+    obs = torch.tensor(obs_list, dtype=torch.float64, device=dev).reshape(-1, 3)
+    p = lambda t: C.c_void_p(t.data_ptr())                      # noqa: E731
+    fl = []
+    for f in range(fleets_max):
+        start = ((idx * 628 + f * 628 // fleets_max) // B % 628).astype(np.int32)   # one period: 628 rows
+        xr0, _ = rmpc.batch.figure8_batch(start * 0.02, 1)
+        x0 = xr0[:, 0] + W.noise_at(idx, W.fleet_seed(1, f))
+        fl.append(dict(start=torch.from_numpy(start).to(dev), x0=torch.from_numpy(x0).to(dev),
+                       states=torch.empty(B, K + 1, 3, dtype=torch.float64, device=dev),
+                       controls=torch.empty(B, K, 2, dtype=torch.float64, device=dev),
+                       cnt=torch.zeros(4, dtype=torch.int64, device=dev),
+                       stream=torch.cuda.Stream(device=dev), ctx=nat.context(dev.index or 0, 16 + f)))
+    rp = nat.RolloutParams()
+    rp.mode, rp.steps, rp.table_len, rp.mpc_rate, rp.plant_method = 1, K, 1000, 1, 0
+    rp.dt, rp.A, rp.a, rp.v_max, rp.omega_max = 0.02, 2.0, 0.5, 2.0, 3.0
+    torch.cuda.synchronize()
+    res, states = {}, {}
+    for S in (1, fleets_max):
+        for warm in (False, True):
+            for f in fl[:S]:
+                nat.check(lib.rmpc_ctx_set_warm_start(f["ctx"], int(warm)), "rmpc_ctx_set_warm_start")
+
+            def run():
+                for f in fl[:S]:
+                    nat.check(lib.rmpc_rollout_batch_dev(f["ctx"], C.byref(rp), None, C.byref(mp), None, B,
+                                                         p(f["start"]), p(f["x0"]), p(obs), obs.shape[0],
+                                                         p(f["states"]), p(f["controls"]), None, p(f["cnt"]),
+                                                         C.c_void_p(f["stream"].cuda_stream)),
+                              "rmpc_rollout_batch_dev")
+            run()
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(3):
+                t = time.perf_counter()
+                run()
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t)
+            res[f"{'warm' if warm else 'cold'}_{S}_fleet{'s' if S > 1 else ''}"] = S * B * K / float(np.median(ts))
+            states.setdefault(warm, fl[0]["states"].cpu().numpy())
+            assert int(fl[0]["cnt"][0].item()) == B * K          # every solve certified optimal
+    for f in fl:
+        nat.check(lib.rmpc_ctx_set_warm_start(f["ctx"], 0), "rmpc_ctx_set_warm_start")
+    res.update({
+        "unit": "solves/s",
+        "workload": f"run_simulation.py MPC loop on the device (rmpc_rollout_batch_dev, mpc_rate 1, config 3's "
+                    f"QP): {B} robots per fleet x {K} steps, seeded noisy starts over one Figure-8 period; "
+                    f"fleets in flight on their own contexts and streams",
+        "warm_start": "rmpc_ctx_set_warm_start: each solve starts from the robot's previous certified sets "
+                      "shifted one step, first-stage cap 2 (library default with warm sets)",
+        "max_abs_state_diff_warm_vs_cold": float(np.abs(states[True] - states[False]).max())})
+    return res
 
 
 def _timed(args, step, dist, dev, S=1):

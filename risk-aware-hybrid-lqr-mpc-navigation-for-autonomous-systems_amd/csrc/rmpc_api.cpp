@@ -90,6 +90,12 @@ struct RmpcCtx {
     bool timed = false;
     int fast_cap = 0, tail_cap = 0;   // rmpc_ctx_set_stage_caps (0: library default)
     bool use_side = true;             // rmpc_ctx_set_side_stream
+    // rmpc_ctx_set_warm_start: per-robot active sets of each robot's previous solve
+    // (MpcFastArgs::prev_sets), valid for the batch shape warm_B / warm_key they were made for
+    bool warm_on = false;
+    DevBuf warm_sets;
+    int64_t warm_B = -1;
+    int64_t warm_key = -1;
     // retry_count: two sets of list counters (RMPC_COUNT_WORDS words at word 0 and 32), used
     // by alternate pipelines; set k is zero in stream order when counts_zero[k] (the
     // previous pipeline's lane-per-robot kernel zeroed it), so the next needs no fill launch
@@ -277,6 +283,7 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     c->retry_sets_b.release();
     c->refine.release();
     c->refine_sets.release();
+    c->warm_sets.release();
     for (DevBuf *d : {&c->ro_x, &c->ro_xr, &c->ro_ur, &c->ro_u, &c->ro_step, &c->ro_cache, &c->ro_prev,
                       &c->ro_since, &c->ro_status, &c->ro_used, &c->ro_risk, &c->ro_counts, &c->ro_off, &c->ro_pred})
         d->release();
@@ -328,6 +335,17 @@ int rmpc_ctx_set_side_stream(RmpcCtx *c, int32_t on) {
     if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
     c->use_side = on != 0;
     for (auto &sc : c->sub) sc->use_side = on != 0;
+    return RMPC_OK;
+}
+
+int rmpc_ctx_set_warm_start(RmpcCtx *c, int32_t on) {
+    if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
+    c->warm_on = on != 0;
+    c->warm_B = -1;                   // (re)start from the cold sets
+    for (auto &sc : c->sub) {
+        sc->warm_on = on != 0;
+        sc->warm_B = -1;
+    }
     return RMPC_OK;
 }
 
@@ -480,7 +498,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                       const double *obstacles, int32_t n_obs, int32_t *step_count, double *u0,
                       double *u_seq, double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
                       int32_t *iters, const int32_t *index, const int32_t *count, hipStream_t s,
-                      const int32_t *ref_off = nullptr, int fast_cap = 0) {
+                      const int32_t *ref_off = nullptr, int fast_cap = 0, int warm_shift = 0) {
     const int bs = p->formulation == RMPC_LTV ? p->block_size : 1;
     const MpcLayout L = rmpc_mpc_layout(p->horizon, bs, n_obs);
     HIP_TRY(ensure_ws(c, L, B));
@@ -565,6 +583,30 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         if (warm) {
             HIP_TRY(c->retry_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
             a.retry_sets = (uint32_t *)c->retry_sets.p;
+        }
+        // warm start across calls (rmpc_ctx_set_warm_start; whole-batch calls, warm_shift steps
+        // since the previous solve): the robots' previous certified sets, zero (= the cold start)
+        // whenever the batch shape differs from the previous call's
+        if (c->warm_on && warm_shift > 0 && !index) {
+            const size_t words = (size_t)B * (size_t)(p->horizon + nb);
+            const int64_t key = (int64_t)p->horizon | (int64_t)nb << 8 | (int64_t)n_obs << 16 |
+                                (int64_t)lti << 24 | (int64_t)f32 << 25;
+            HIP_TRY(c->warm_sets.ensure(words * sizeof(uint32_t)));
+            if (c->warm_B != B || c->warm_key != key) {
+                HIP_TRY(hipMemsetAsync(c->warm_sets.p, 0, words * sizeof(uint32_t), s));
+                c->warm_B = B;
+                c->warm_key = key;
+            }
+            a.prev_sets = (uint32_t *)c->warm_sets.p;
+            a.prev_shift = warm_shift;
+            // From warm sets most robots certify in their first or second solve, and a robot
+            // still iterating after two is one of the few hard ones: the tail's lane groups take
+            // it sooner (config-3 closed loop, 65536 robots: 190M -> 274M solves/s, three fleets
+            // in flight 407M -> 498M; profiles/r03/closed_loop_warm.txt).  fp64 LTV at N <= 20;
+            // the caller's caps win.
+            if (!rmpc_knob("RMPC_FAST_CAP") && fast_cap <= 0 && c->fast_cap <= 0 && !lti && !f32 &&
+                p->horizon <= 20)
+                a.pdas_cap = 2;
         }
         // RMPC_DENSE_PROF=1: per-phase cycle counters of the fast and dense kernels to
         // stderr (synchronises the stream; diagnostics only)
@@ -689,7 +731,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                                                         uref_rows, obstacles, step_count, u0, u_seq, x_pred, cost,
                                                         status, slack_used, iters, left, left_n,
                                                         (int32_t *)c->retry2.p, cnt2, tail_cap, a.retry_sets, s, pc,
-                                                        tail32, lti, &c->gdiag);
+                                                        tail32, lti, &c->gdiag, a.prev_sets);
             // join the refinement before anything else, also when the tail's launch failed (the
             // call's stream must not complete ahead of the side branch)
             if (refine_side) HIP_TRY(hipStreamWaitEvent(s, c->rev[1], 0));
@@ -699,7 +741,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                                               obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
                                               iters, (const int32_t *)c->retry_r.p, cnt + 10, (int32_t *)c->retry2.p,
                                               cnt2, tail_cap, (const uint32_t *)c->retry_sets_r.p, s, pc, tail32, lti,
-                                              &c->gdiag));
+                                              &c->gdiag, a.prev_sets));
             }
             if (prof) {
                 unsigned long long h[64];
@@ -860,7 +902,8 @@ extern "C" int rmpc_mpc_solve_batch_dev(RmpcCtx *c, const RmpcMpcParams *p, int6
         return fail(RMPC_EINVAL, "required pointer is NULL");
     HIP_TRY(hipSetDevice(c->device));
     return launch_mpc(c, p, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs, step_count, u0,
-                      u_seq, x_pred, cost, status, slack_used, iters, nullptr, nullptr, pick(c, stream));
+                      u_seq, x_pred, cost, status, slack_used, iters, nullptr, nullptr, pick(c, stream), nullptr, 0,
+                      1);
 }
 
 extern "C" int rmpc_mpc_solve_batch(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const double *x0,
@@ -1323,8 +1366,9 @@ extern "C" int rmpc_rollout_batch_dev(RmpcCtx *c, const RmpcRolloutParams *rp, c
                                             nullptr, nullptr, nullptr, s));
         } else if (mode == 1) {                            // :250-259, zero-order hold in u
             if (k % rp->mpc_rate == 0) {
+                // (warm start on the context: from each robot's solve mpc_rate steps earlier)
                 RC(launch_mpc(c, mp, B, x, xr, rows, ur, rows, obstacles, n_obs, step, u, nullptr, nullptr,
-                              nullptr, status, nullptr, nullptr, nullptr, nullptr, s, off));
+                              nullptr, status, nullptr, nullptr, nullptr, nullptr, s, off, 0, rp->mpc_rate));
                 HIP_TRY(rmpc_launch_status_count(B, status, nullptr, counts, s));
             }
         } else {                                           // :525-559

@@ -201,7 +201,11 @@ template <> struct Big<float> { static constexpr float v = 1e30f; };
 // across the pair with one DPP swap (a + b on one lane, b + a on the other: identical).
 // Used where the rows dominate a step (8 obstacles) and the batch fills only half the SIMDs
 // at one lane per robot (BASELINE config 4: 32768 robots = 512 waves).
-template <int N, int BS, typename T, bool LTI, int NO = 0, int PR = 1>
+//
+// WS: the warm start across calls (MpcFastArgs::prev_sets) is compiled in.  Config 3's instance
+// is built both ways and the cold one launched when prev_sets is null: the read and write-back
+// cost its register allocation ~1% (profiles/r03/ab_warm_start.txt).
+template <int N, int BS, typename T, bool LTI, int NO = 0, int PR = 1, bool WS = true>
 __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     static_assert(!LTI || BS == 1, "LTI ignores move blocking");
     static_assert(PR == 1 || (PR == 2 && NO > 0 && NO % 2 == 0 && BS == 1 && !LTI && NO / 2 <= 4),
@@ -440,6 +444,29 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         for (int j = 0; j < NB; j++) Bf.set(j, ws[(N + j) * a.B]);
         it = (int)ws[(N + NB) * a.B];
         if (it > 0) hist0 = set_sig();
+    } else if (WS && a.prev_sets) {
+        // Warm start from this robot's previous solve (rmpc_ctx_set_warm_start): the PDAS
+        // counterpart of the reference's warm_start=True with get_warm_start's one-step shift
+        // (mpc_controller.py:272-277, 470-475, 524-538).  Its certified sets, shifted by
+        // prev_shift steps with the last step repeated, are the first iterate's sets; the QP and
+        // its optimum are unchanged (the outputs come from the certified sets only).
+        const uint32_t *ws = a.prev_sets + b;
+        const int sh = a.prev_shift, shb = a.prev_shift / BS;
+        const uint32_t hm = PR == 2 ? ((1u << NOL) - 1u) : (no >= 16 ? 0xffffu : ((1u << no) - 1u));
+#pragma unroll
+        for (int k = 1; k < N; k++) {
+            const int ks = k + sh < N ? k + sh : N - 1;
+            const uint32_t w = ws[(size_t)ks * a.B];
+            Hf.set(k, (PR == 2 ? (w >> obase) : w) & hm);
+        }
+#pragma unroll
+        for (int j = 0; j < NB; j++) {
+            const int js = j + shb < NB ? j + shb : NB - 1;
+            uint32_t v = ws[(size_t)(N + js) * a.B] & 0xfu;
+            if ((v & 3u) == 3u) v &= ~3u;           // (never both bounds of a component)
+            if ((v & 12u) == 12u) v &= ~12u;
+            Bf.set(j, v);
+        }
     }
 #ifndef RMPC_INIT_ZC_BUILD
 #define RMPC_INIT_ZC_BUILD 1
@@ -1032,6 +1059,15 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     // u = u_refs + du, omega ramp, step counter.  In fp32 the fp64 references are re-read so
     // that only the deviations carry fp32 rounding.
     // LTI: u = du (no u_ref), x_pred = e + x_ref (absolute), no ramp or step count.
+    if constexpr (PR == 2) {               // warm start: the pair's combined row flags
+        if (WS && a.prev_sets) {
+#pragma unroll
+            for (int i = 0; i < (N + 1) / 2; i++) {
+                const uint32_t w = Hf.w[i], o = pair_xchg(w);
+                Hf.w[i] = pp ? (o | (w << NOL)) : (w | (o << NOL));
+            }
+        }
+    }
     if (PR == 2 && pp) return;             // paired lanes: lane 2r writes the outputs
     const unsigned long long t_out0 = a.prof ? __builtin_amdgcn_s_memtime() : 0ull;   // (diagnostics)
 #pragma unroll
@@ -1129,6 +1165,13 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     if (a.slack_used) a.slack_used[b] = (uint8_t)used;
     a.status[b] = RMPC_OPTIMAL;
     if (a.iters) a.iters[b] = it;
+    if (WS && a.prev_sets) {               // warm start of this robot's next solve: its certified sets
+        uint32_t *ws = a.prev_sets + b;
+#pragma unroll
+        for (int k = 0; k < N; k++) ws[(size_t)k * a.B] = Hf.get(k);
+#pragma unroll
+        for (int j = 0; j < NB; j++) ws[(size_t)(N + j) * a.B] = Bf.get(j);
+    }
     if (a.prof) {
         const unsigned long long t_end = __builtin_amdgcn_s_memtime();
         atomicMax(a.prof + 23, t_end - t_entry);
@@ -1194,7 +1237,8 @@ hipError_t rmpc_launch_mpc_fast(const MpcFastArgs &a, int N, int bs, int prec, h
         // (N = 30, 8 obstacles in fp64: paired lanes -- fp64 requests and the fp32 requests'
         // refinement pass)
         if (bs == 1 && N == 30 && a.no == 8) hipLaunchKernelGGL((mpc_ltv_fast_kernel<30, 1, double, false, 8, 2>), grid2, block, lds2, stream, a);
-        else if (bs == 1 && N == 20 && a.no == 3 && !nospec) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, false, 3>), grid, block, lds, stream, a);
+        else if (bs == 1 && N == 20 && a.no == 3 && !nospec && a.prev_sets) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, false, 3>), grid, block, lds, stream, a);
+        else if (bs == 1 && N == 20 && a.no == 3 && !nospec) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, false, 3, 1, false>), grid, block, lds, stream, a);
         else if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, false>), grid, block, lds, stream, a);
         else if (bs == 1 && N == 10) hipLaunchKernelGGL((mpc_ltv_fast_kernel<10, 1, double, false>), grid, block, lds, stream, a);
         else if (bs == 1 && N == 6) hipLaunchKernelGGL((mpc_ltv_fast_kernel<6, 1, double, false>), grid, block, lds, stream, a);

@@ -1,0 +1,82 @@
+"""Closed-loop MPC throughput with and without the warm start across calls
+(rmpc_ctx_set_warm_start; the reference's warm_start=True solves, mpc_controller.py:272-277,
+524-538).  Each fleet of B robots runs run_simulation.py's MPC loop on the device
+(rmpc_rollout_batch_dev, mpc_rate 1: one solve_with_ltv per robot and control step, then the
+plant), from seeded noisy starts spread over one Figure-8 period.  S fleets run at once, each on
+its own context and stream (one fleet's closed loop cannot overlap its own steps; independent
+fleets can, as bench.py's batches in flight).  Prints one JSON line per (S, warm) and the largest
+state difference between the warm and cold closed loops.
+Usage: python scripts/closed_loop_warm.py [B] [steps] [S ...]   (CL_CAPS="f,t;f,t..." also times
+the warm loop under other stage caps, rmpc_ctx_set_stage_caps)"""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                "risk-aware-hybrid-lqr-mpc-navigation-for-autonomous-systems_amd"))
+import rmpc                                                     # noqa: E402
+from rmpc import _native as nat                                 # noqa: E402
+from rmpc import workloads as W                                 # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+K = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+SS = [int(v) for v in sys.argv[3:]] or [1, 3]
+dev = torch.device("cuda:0")
+lib = nat.load()
+mp = nat.mpc_params(20, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+idx = np.arange(B)
+obs = torch.tensor(W.DEFAULT_OBS, dtype=torch.float64, device=dev)
+p = lambda t: C.c_void_p(t.data_ptr())                          # noqa: E731
+fleets = []
+for f in range(max(SS)):
+    start_h = ((idx * 628 + f * 628 // max(SS)) // B % 628).astype(np.int32)   # one Figure-8 period
+    xr0, _ = rmpc.batch.figure8_batch(start_h * 0.02, 1)
+    x0_h = xr0[:, 0] + W.noise_at(idx, W.fleet_seed(1, f))
+    fleets.append(dict(start=torch.from_numpy(start_h).to(dev), x0=torch.from_numpy(x0_h).to(dev),
+                       states=torch.empty(B, K + 1, 3, dtype=torch.float64, device=dev),
+                       controls=torch.empty(B, K, 2, dtype=torch.float64, device=dev),
+                       cnt=torch.zeros(4, dtype=torch.int64, device=dev),
+                       stream=torch.cuda.Stream(device=dev), ctx=nat.context(0, 4 + f)))
+rp = nat.RolloutParams()
+rp.mode, rp.steps, rp.table_len, rp.mpc_rate, rp.plant_method = 1, K, 1000, 1, 0
+rp.dt, rp.A, rp.a, rp.v_max, rp.omega_max = 0.02, 2.0, 0.5, 2.0, 3.0
+torch.cuda.synchronize()
+res = {}
+runs = [(False, "0,0"), (True, "0,0")] + [(True, c) for c in os.environ.get("CL_CAPS", "").split(";") if c]
+for S in SS:
+    for warm, caps in runs:
+        for fl in fleets[:S]:
+            nat.check(lib.rmpc_ctx_set_warm_start(fl["ctx"], int(warm)), "rmpc_ctx_set_warm_start")
+            nat.check(lib.rmpc_ctx_set_stage_caps(fl["ctx"], *[int(v) for v in caps.split(",")]),
+                      "rmpc_ctx_set_stage_caps")
+
+        def run():
+            for fl in fleets[:S]:
+                nat.check(lib.rmpc_rollout_batch_dev(fl["ctx"], C.byref(rp), None, C.byref(mp), None, B,
+                                                     p(fl["start"]), p(fl["x0"]), p(obs), 3, p(fl["states"]),
+                                                     p(fl["controls"]), None, p(fl["cnt"]),
+                                                     C.c_void_p(fl["stream"].cuda_stream)),
+                          "rmpc_rollout_batch_dev")
+        run()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(3):
+            t = time.perf_counter()
+            run()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t)
+        t = float(np.median(ts))
+        res.setdefault((S, warm), fleets[0]["states"].cpu().numpy())
+        _ = fleets[0]["states"].cpu().numpy()
+        print(json.dumps({"fleets_in_flight": S, "warm_start": warm, "stage_caps": caps, "robots_per_fleet": B, "steps": K, "s": t,
+                          "mpc_solves_per_s": S * B * K / t, "ms_per_step": t / K * 1e3,
+                          "mpc_status_fleet0": fleets[0]["cnt"].cpu().tolist()}), flush=True)
+    for fl in fleets:
+        nat.check(lib.rmpc_ctx_set_warm_start(fl["ctx"], 0), "rmpc_ctx_set_warm_start")
+    print(json.dumps({"fleets_in_flight": S, "max_abs_state_diff_warm_vs_cold":
+                      float(np.abs(res[(S, True)] - res[(S, False)]).max())}), flush=True)

@@ -822,3 +822,87 @@ def test_side_stream_on_off_bitwise_identical(rm):
     for a, b in zip(h1, h0):
         for x, y in zip(a, b):
             np.testing.assert_array_equal(x, y)
+
+
+def _closed_loop_warm_vs_cold(rm, p, B, steps, obs, seed, N, slot=3):
+    """One closed loop driven by the cold-started solves (slot 0) while a warm-started context
+    (`slot`) solves the same inputs each step; returns per-step outputs of both."""
+    from rmpc import workloads as W
+    idx = np.arange(B)
+    t0 = W.t0_at(idx, B)
+    xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, t0, N + 1)
+    x = xr[:, 0] + W.noise_at(idx, seed)
+    sc_c, sc_w = np.full(B, 10, np.int32), np.full(B, 10, np.int32)
+    res = []
+    for k in range(steps):
+        xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, t0 + k * 0.02, N + 1)
+        c = rm.batch.mpc_solve_batch(p, x, xr, ur, obs, step_count=sc_c)
+        w = rm.batch.mpc_solve_batch(p, x, xr, ur, obs, step_count=sc_w, slot=slot)
+        res.append((c, w))
+        x = rm.batch.plant_step_batch(x, c["u0"], 0.02, 2.0, 3.0)
+    return res
+
+
+def test_mpc_warm_start_closed_loop_same_optimum(rm, capsys):
+    """rmpc_ctx_set_warm_start, the counterpart of the reference's warm_start=True solves and
+    get_warm_start's one-step shift (mpc_controller.py:272-277, 470-475, 524-538): along a
+    closed loop, each robot's solve starts from its previous solve's certified sets shifted by
+    one step.  The QP is unchanged, so every output equals the cold-started solve's
+    (|du|, |dx| <= 1e-9, same status); only the PDAS iteration count drops.
+    - config 3's shape (fp64, N = 20, 3 obstacles), 4096 robots x 25 steps;
+    - config 4's (fp32 request: the paired-lane fp32 pass reads the sets, the fp64 refinement
+      writes them), 2048 robots x 8 steps;
+    - with warm sets the first stage stops after 2 solves by default (the few robots still
+      iterating go to the lane-group tail): same optimum;
+    - a call of another batch size on the warm context starts cold (same iterations as cold
+      under the same caps);
+    - an MPC rollout on a warm context reproduces the cold rollout (mpc_rate 1 and 5)."""
+    from rmpc import workloads as W
+    p3 = rm._native.mpc_params(20, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+    p4 = rm._native.mpc_params(30, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02,
+                               block_size=1, precision=1)
+    try:
+        rm.batch.set_warm_start(True, slot=3)
+        for tag, p, B, steps, obs, N in (("cfg3", p3, 4096, 25, ompc.default_obstacles(), 20),
+                                         ("cfg4", p4, 2048, 8, W.UNION8_OBS, 30)):
+            rm.batch.set_warm_start(True, slot=3)          # (resets the sets)
+            res = _closed_loop_warm_vs_cold(rm, p, B, steps, obs, 1, N)
+            it_c = it_w = 0
+            for k, (c, w) in enumerate(res):
+                np.testing.assert_array_equal(c["status"], w["status"])
+                assert np.all(c["status"] == 0), (tag, k)
+                assert np.abs(c["u_seq"] - w["u_seq"]).max() <= 1e-9, (tag, k)
+                assert np.abs(c["x_pred"] - w["x_pred"]).max() <= 1e-9, (tag, k)
+                if k > 0:
+                    it_c += int(c["iters"].sum())
+                    it_w += int(w["iters"].sum())
+            with capsys.disabled():
+                print(f"\n[warm start {tag}] PDAS solves per robot-step after the first: cold "
+                      f"{it_c / (B * (steps - 1)):.3f}, warm {it_w / (B * (steps - 1)):.3f}")
+            assert it_w < 0.8 * it_c, (tag, it_w, it_c)
+        # another shape on the warm context: cold sets again (the cold pipeline's caps, so
+        # that the iteration counts compare; a warm context's default first-stage cap is 2)
+        rm.batch.set_stage_caps(7, 4, slot=3)
+        idx = np.arange(1024)
+        xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, W.t0_at(idx, 1024), 21)
+        x0 = xr[:, 0] + W.noise_at(idx, 5)
+        c = rm.batch.mpc_solve_batch(p3, x0, xr, ur, ompc.default_obstacles(), step_count=np.full(1024, 10, np.int32))
+        w = rm.batch.mpc_solve_batch(p3, x0, xr, ur, ompc.default_obstacles(), step_count=np.full(1024, 10, np.int32),
+                                     slot=3)
+        for k in ("u0", "u_seq", "x_pred", "status", "iters"):
+            np.testing.assert_array_equal(c[k], w[k])
+        rm.batch.set_stage_caps(0, 0, slot=3)
+        # MPC rollouts: the same closed loop warm or cold
+        start = (np.arange(2048) * 7) % 900
+        for rate in (1, 5):
+            ro = {}
+            for on in (False, True):
+                rm.batch.set_warm_start(on, slot=3)
+                ro[on] = rm.batch.rollout_batch("mpc", 60, mparams=p3, start_index=start,
+                                                obstacles=ompc.default_obstacles(), mpc_rate=rate, slot=3)
+            assert ro[True]["mpc_status"][0] == ro[False]["mpc_status"][0] > 0
+            assert np.abs(ro[True]["states"] - ro[False]["states"]).max() <= 1e-9, rate
+            assert np.abs(ro[True]["controls"] - ro[False]["controls"]).max() <= 1e-9, rate
+    finally:
+        rm.batch.set_warm_start(False, slot=3)
+        rm.batch.set_stage_caps(0, 0, slot=3)
