@@ -385,8 +385,8 @@ def main():
 
     # ---- closed loop (rank 0, N=1, config 3 only; never `value`): run_simulation.py's MPC loop
     # on the device, cold and with the warm start across calls (rmpc_ctx_set_warm_start)
-    if world == 1 and rank == 0 and args.config == "cfg3" and not args.lti and not f32 and not args.no_closed_loop:
-        line["closed_loop"] = closed_loop(dev, B, obs_list)
+    if world == 1 and rank == 0 and args.config in ("cfg3", "cfg4") and not args.lti and not args.no_closed_loop:
+        line["closed_loop"] = closed_loop(dev, B, obs_list, N, f32)
 
     # ---- CPU baseline (rank 0, N=1 only): the oracle's C restatement of the same algorithm
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
@@ -471,7 +471,7 @@ def main():
 
 
 
-def closed_loop(dev, B, obs_list, K=50, fleets_max=3):
+def closed_loop(dev, B, obs_list, N=20, f32=False, K=50, fleets_max=3):
     """run_simulation.py's MPC loop (mpc_rate 1: one solve_with_ltv per robot and control step,
     then the plant) for fleets of B robots on the device (rmpc_rollout_batch_dev), from seeded
     noisy starts over one Figure-8 period; 1 and `fleets_max` fleets at once (one context and
@@ -487,7 +487,8 @@ def closed_loop(dev, B, obs_list, K=50, fleets_max=3):
     from rmpc import _native as nat
     from rmpc import workloads as W
     lib = nat.load()
-    mp = nat.mpc_params(20, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+    mp = nat.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02,
+                        precision=1 if f32 else 0)
     idx = np.arange(B)
     obs = torch.tensor(obs_list, dtype=torch.float64, device=dev).reshape(-1, 3)
     p = lambda t: C.c_void_p(t.data_ptr())                      # noqa: E731
@@ -533,11 +534,12 @@ def closed_loop(dev, B, obs_list, K=50, fleets_max=3):
         nat.check(lib.rmpc_ctx_set_warm_start(f["ctx"], 0), "rmpc_ctx_set_warm_start")
     res.update({
         "unit": "solves/s",
-        "workload": f"run_simulation.py MPC loop on the device (rmpc_rollout_batch_dev, mpc_rate 1, config 3's "
-                    f"QP): {B} robots per fleet x {K} steps, seeded noisy starts over one Figure-8 period; "
-                    f"fleets in flight on their own contexts and streams",
+        "workload": f"run_simulation.py MPC loop on the device (rmpc_rollout_batch_dev, mpc_rate 1, the config's "
+                    f"QP, N={N}, {obs.shape[0]} obstacles{', fp32 request' if f32 else ''}): {B} robots per fleet x "
+                    f"{K} steps, seeded noisy starts over one Figure-8 period; fleets in flight on their own "
+                    f"contexts and streams",
         "warm_start": "rmpc_ctx_set_warm_start: each solve starts from the robot's previous certified sets "
-                      "shifted one step, first-stage cap 2 (library default with warm sets)",
+                      f"shifted one step, first-stage cap {4 if f32 else 2} (library default with warm sets)",
         "max_abs_state_diff_warm_vs_cold": float(np.abs(states[True] - states[False]).max())})
     return res
 

@@ -28,9 +28,12 @@ K = int(sys.argv[2]) if len(sys.argv) > 2 else 50
 SS = [int(v) for v in sys.argv[3:]] or [1, 3]
 dev = torch.device("cuda:0")
 lib = nat.load()
-mp = nat.mpc_params(20, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+# CL_CFG=cfg4: config 4's QP (N = 30, the union-8 obstacles, fp32 request) instead of config 3's
+cfg4 = os.environ.get("CL_CFG", "cfg3") == "cfg4"
+mp = nat.mpc_params(30 if cfg4 else 20, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02,
+                    precision=1 if cfg4 else 0)
 idx = np.arange(B)
-obs = torch.tensor(W.DEFAULT_OBS, dtype=torch.float64, device=dev)
+obs = torch.tensor(W.UNION8_OBS if cfg4 else W.DEFAULT_OBS, dtype=torch.float64, device=dev)
 p = lambda t: C.c_void_p(t.data_ptr())                          # noqa: E731
 fleets = []
 for f in range(max(SS)):
@@ -58,7 +61,7 @@ for S in SS:
         def run():
             for fl in fleets[:S]:
                 nat.check(lib.rmpc_rollout_batch_dev(fl["ctx"], C.byref(rp), None, C.byref(mp), None, B,
-                                                     p(fl["start"]), p(fl["x0"]), p(obs), 3, p(fl["states"]),
+                                                     p(fl["start"]), p(fl["x0"]), p(obs), obs.shape[0], p(fl["states"]),
                                                      p(fl["controls"]), None, p(fl["cnt"]),
                                                      C.c_void_p(fl["stream"].cuda_stream)),
                           "rmpc_rollout_batch_dev")
