@@ -471,7 +471,7 @@ def main():
 
 
 
-def closed_loop(dev, B, obs_list, N=20, f32=False, K=50, fleets_max=3):
+def closed_loop(dev, B, obs_list, N=20, f32=False, K=50, fleets_max=3, hybrid=False, t0=None):
     """run_simulation.py's MPC loop (mpc_rate 1: one solve_with_ltv per robot and control step,
     then the plant) for fleets of B robots on the device (rmpc_rollout_batch_dev), from seeded
     noisy starts over one Figure-8 period; 1 and `fleets_max` fleets at once (one context and
@@ -493,8 +493,13 @@ def closed_loop(dev, B, obs_list, N=20, f32=False, K=50, fleets_max=3):
     obs = torch.tensor(obs_list, dtype=torch.float64, device=dev).reshape(-1, 3)
     p = lambda t: C.c_void_p(t.data_ptr())                      # noqa: E731
     fl = []
+    lp = nat.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0)
+    kp = nat.risk_params()
     for f in range(fleets_max):
-        start = ((idx * 628 + f * 628 // fleets_max) // B % 628).astype(np.int32)   # one period: 628 rows
+        if t0 is None:
+            start = ((idx * 628 + f * 628 // fleets_max) // B % 628).astype(np.int32)   # one period: 628 rows
+        else:                              # the config's own time offsets (config 5: near obstacles)
+            start = ((np.rint(np.asarray(t0) / 0.02).astype(np.int64) + f) % 628).astype(np.int32)
         xr0, _ = rmpc.batch.figure8_batch(start * 0.02, 1)
         x0 = xr0[:, 0] + W.noise_at(idx, W.fleet_seed(1, f))
         fl.append(dict(start=torch.from_numpy(start).to(dev), x0=torch.from_numpy(x0).to(dev),
@@ -503,7 +508,7 @@ def closed_loop(dev, B, obs_list, N=20, f32=False, K=50, fleets_max=3):
                        cnt=torch.zeros(4, dtype=torch.int64, device=dev),
                        stream=torch.cuda.Stream(device=dev), ctx=nat.context(dev.index or 0, 16 + f)))
     rp = nat.RolloutParams()
-    rp.mode, rp.steps, rp.table_len, rp.mpc_rate, rp.plant_method = 1, K, 1000, 1, 0
+    rp.mode, rp.steps, rp.table_len, rp.mpc_rate, rp.plant_method = 2 if hybrid else 1, K, 1000, 1, 0
     rp.dt, rp.A, rp.a, rp.v_max, rp.omega_max = 0.02, 2.0, 0.5, 2.0, 3.0
     torch.cuda.synchronize()
     res, states = {}, {}
@@ -514,7 +519,8 @@ def closed_loop(dev, B, obs_list, N=20, f32=False, K=50, fleets_max=3):
 
             def run():
                 for f in fl[:S]:
-                    nat.check(lib.rmpc_rollout_batch_dev(f["ctx"], C.byref(rp), None, C.byref(mp), None, B,
+                    nat.check(lib.rmpc_rollout_batch_dev(f["ctx"], C.byref(rp), C.byref(lp) if hybrid else None,
+                                                         C.byref(mp), C.byref(kp) if hybrid else None, B,
                                                          p(f["start"]), p(f["x0"]), p(obs), obs.shape[0],
                                                          p(f["states"]), p(f["controls"]), None, p(f["cnt"]),
                                                          C.c_void_p(f["stream"].cuda_stream)),
@@ -529,12 +535,13 @@ def closed_loop(dev, B, obs_list, N=20, f32=False, K=50, fleets_max=3):
                 ts.append(time.perf_counter() - t)
             res[f"{'warm' if warm else 'cold'}_{S}_fleet{'s' if S > 1 else ''}"] = S * B * K / float(np.median(ts))
             states.setdefault(warm, fl[0]["states"].cpu().numpy())
-            assert int(fl[0]["cnt"][0].item()) == B * K          # every solve certified optimal
+            cnt = fl[0]["cnt"].cpu().numpy()
+            assert cnt[1:].sum() == 0 and (hybrid or cnt[0] == B * K)   # every solve certified optimal
     for f in fl:
         nat.check(lib.rmpc_ctx_set_warm_start(f["ctx"], 0), "rmpc_ctx_set_warm_start")
     res.update({
         "unit": "solves/s",
-        "workload": f"run_simulation.py MPC loop on the device (rmpc_rollout_batch_dev, mpc_rate 1, the config's "
+        "workload": f"run_simulation.py {'hybrid' if hybrid else 'MPC'} loop on the device (rmpc_rollout_batch_dev, mpc_rate 1, the config's "
                     f"QP, N={N}, {obs.shape[0]} obstacles{', fp32 request' if f32 else ''}): {B} robots per fleet x "
                     f"{K} steps, seeded noisy starts over one Figure-8 period; fleets in flight on their own "
                     f"contexts and streams",
@@ -755,6 +762,12 @@ def bench_other(args, world, rank, local, dist, pre=None):
         fm = float(used_h.mean())
         line["mpc_fraction"] = fm
         line["kernel_avg_ms"] = k_avg_s * 1e3
+        # closed loop (rank 0, N=1; never `value`): run_simulation.py's hybrid loop on the device,
+        # cold and with the warm start across calls (the MPC branch's robots, per-robot stamps)
+        if world == 1 and rank == 0 and not args.no_closed_loop:
+            line["closed_loop"] = closed_loop(dev, B, W.DEFAULT_OBS, N, False, hybrid=True, t0=W.cfg5_t0(idx))
+            line["closed_loop"]["unit"] = "hybrid control steps/s"
+
         # risk 10 n_o + the chosen branch's canonical work per robot
         # (MPC: condensed-QP model at the MPC robots' mean iterations; LQR: 6e3)
         its_mpc = None

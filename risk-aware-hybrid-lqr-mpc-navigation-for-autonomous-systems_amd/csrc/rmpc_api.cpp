@@ -96,6 +96,7 @@ struct RmpcCtx {
     DevBuf warm_sets;
     int64_t warm_B = -1;
     int64_t warm_key = -1;
+    uint32_t warm_calls = 0;          // stamp of the last warm call (MpcFastArgs::prev_stamp)
     // retry_count: two sets of list counters (RMPC_COUNT_WORDS words at word 0 and 32), used
     // by alternate pipelines; set k is zero in stream order when counts_zero[k] (the
     // previous pipeline's lane-per-robot kernel zeroed it), so the next needs no fill launch
@@ -584,11 +585,12 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             HIP_TRY(c->retry_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
             a.retry_sets = (uint32_t *)c->retry_sets.p;
         }
-        // warm start across calls (rmpc_ctx_set_warm_start; whole-batch calls, warm_shift steps
-        // since the previous solve): the robots' previous certified sets, zero (= the cold start)
-        // whenever the batch shape differs from the previous call's
-        if (c->warm_on && warm_shift > 0 && !index) {
-            const size_t words = (size_t)B * (size_t)(p->horizon + nb);
+        // warm start across calls (rmpc_ctx_set_warm_start; warm_shift steps since the previous
+        // call): the robots' previous certified sets, used by a robot whose last solve was the
+        // previous call (stamps; the hybrid step's MPC branch takes a different subset each
+        // step), zero (= the cold start) whenever the batch shape differs from the previous call's
+        if (c->warm_on && warm_shift > 0) {
+            const size_t words = (size_t)B * (size_t)(p->horizon + nb + 1);
             const int64_t key = (int64_t)p->horizon | (int64_t)nb << 8 | (int64_t)n_obs << 16 |
                                 (int64_t)lti << 24 | (int64_t)f32 << 25;
             HIP_TRY(c->warm_sets.ensure(words * sizeof(uint32_t)));
@@ -596,9 +598,11 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                 HIP_TRY(hipMemsetAsync(c->warm_sets.p, 0, words * sizeof(uint32_t), s));
                 c->warm_B = B;
                 c->warm_key = key;
+                c->warm_calls = 0;
             }
             a.prev_sets = (uint32_t *)c->warm_sets.p;
             a.prev_shift = warm_shift;
+            a.prev_stamp = ++c->warm_calls;
             // From warm sets most robots certify in their first or second solve, and a robot
             // still iterating after a few is one of the few hard ones: the tail's lane groups
             // take it sooner.  fp64 LTV at N <= 20: 2 (config-3 closed loop, 65536 robots: 191M
@@ -733,7 +737,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                                                         uref_rows, obstacles, step_count, u0, u_seq, x_pred, cost,
                                                         status, slack_used, iters, left, left_n,
                                                         (int32_t *)c->retry2.p, cnt2, tail_cap, a.retry_sets, s, pc,
-                                                        tail32, lti, &c->gdiag, a.prev_sets);
+                                                        tail32, lti, &c->gdiag, a.prev_sets, a.prev_stamp);
             // join the refinement before anything else, also when the tail's launch failed (the
             // call's stream must not complete ahead of the side branch)
             if (refine_side) HIP_TRY(hipStreamWaitEvent(s, c->rev[1], 0));
@@ -743,7 +747,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                                               obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
                                               iters, (const int32_t *)c->retry_r.p, cnt + 10, (int32_t *)c->retry2.p,
                                               cnt2, tail_cap, (const uint32_t *)c->retry_sets_r.p, s, pc, tail32, lti,
-                                              &c->gdiag, a.prev_sets));
+                                              &c->gdiag, a.prev_sets, a.prev_stamp));
             }
             if (prof) {
                 unsigned long long h[64];
@@ -1161,7 +1165,7 @@ static int hybrid_step(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams
     const int rc = launch_mpc(c, mp, B, x, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs, step_count, u_out,
                               nullptr, pred, nullptr, (int32_t *)c->hyb_status.p, nullptr, nullptr,
                               (const int32_t *)c->idx_mpc.p, cnt + 1, s, ref_off,
-                              c->fast_cap > 0 ? c->fast_cap : (mp->horizon <= 20 ? 6 : 0));
+                              c->fast_cap > 0 ? c->fast_cap : (mp->horizon <= 20 && !c->warm_on ? 6 : 0), 1);
     if (side) HIP_TRY(hipStreamWaitEvent(s, c->hev[1], 0));   // join: the step ends when both branches have
     return rc;
 }

@@ -77,11 +77,14 @@ struct MpcFastArgs {
     uint32_t *refine_sets;
     int init_zc;                     // cold start: hinge rows violated by the free response start active
     // Warm start across calls (rmpc_ctx_set_warm_start): per ROBOT b, the active sets of its
-    // previous certified solve, slot-minor [N + NB][B] (hinge flags, box states); read shifted
-    // by prev_shift steps at the start (the last step repeated), written back at certification
-    // (this kernel's output pass and the tail's).  All zero = the cold start.  Null: off.
+    // previous certified solve, slot-minor [N + NB + 1][B] (hinge flags, box states, the stamp
+    // of the call that wrote them); read shifted by prev_shift steps at the start (the last step
+    // repeated) when the stamp is prev_stamp - 1 (the robot's last solve was the previous call),
+    // written back with prev_stamp at certification (this kernel's output pass and the tail's).
+    // All zero = the cold start.  Null: off.
     uint32_t *prev_sets;
     int prev_shift;
+    uint32_t prev_stamp;
 };
 // list counters per set of a context (retry_count holds two sets, used by alternate calls)
 #define RMPC_COUNT_WORDS 16
@@ -124,7 +127,8 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
                                  const int32_t *index, const int32_t *count, int32_t *retry,
                                  int32_t *retry_count, int pdas_cap, const uint32_t *warm,
                                  hipStream_t stream, unsigned long long *prof = nullptr, bool f32 = false,
-                                 bool lti = false, GroupDiag *diag = nullptr, uint32_t *prev_sets = nullptr);
+                                 bool lti = false, GroupDiag *diag = nullptr, uint32_t *prev_sets = nullptr,
+                                 uint32_t prev_stamp = 0);
 
 hipError_t rmpc_launch_mpc_f64(const MpcDevParams &prm, const MpcLayout &L, int64_t B,
                                const double *x0, const double *x_refs, int ref_rows,

@@ -444,7 +444,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         for (int j = 0; j < NB; j++) Bf.set(j, ws[(N + j) * a.B]);
         it = (int)ws[(N + NB) * a.B];
         if (it > 0) hist0 = set_sig();
-    } else if (WS && a.prev_sets) {
+    } else if (WS && a.prev_sets && a.prev_sets[(size_t)(N + NB) * a.B + b] + 1u == a.prev_stamp) {
         // Warm start from this robot's previous solve (rmpc_ctx_set_warm_start): the PDAS
         // counterpart of the reference's warm_start=True with get_warm_start's one-step shift
         // (mpc_controller.py:272-277, 470-475, 524-538).  Its certified sets, shifted by
@@ -1171,6 +1171,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
         for (int k = 0; k < N; k++) ws[(size_t)k * a.B] = Hf.get(k);
 #pragma unroll
         for (int j = 0; j < NB; j++) ws[(size_t)(N + j) * a.B] = Bf.get(j);
+        ws[(size_t)(N + NB) * a.B] = a.prev_stamp;
     }
     if (a.prof) {
         const unsigned long long t_end = __builtin_amdgcn_s_memtime();

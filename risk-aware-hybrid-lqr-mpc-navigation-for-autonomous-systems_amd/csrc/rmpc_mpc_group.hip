@@ -72,7 +72,8 @@ struct GroupArgs {
     int32_t *chk;                     // optional bounds-check record (RMPC_GROUP_CHECK, host-mapped)
     int32_t *site;                    // optional per-wave progress words (RMPC_GROUP_CHECK=2, host-mapped)
     uint32_t *prev_sets;              // warm start across calls (MpcFastArgs::prev_sets): per robot,
-                                      // [N + NB][nB]; a certified robot's sets are written back
+                                      // [N + NB + 1][nB]; a certified robot's sets are written back
+    uint32_t prev_stamp;              // ... with this stamp
 };
 
 // RMPC_GROUP_CHECK: an out-of-range index sets a flag bit and (first hit only) records the
@@ -1536,6 +1537,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
             if (a.prev_sets) {             // warm start of this robot's next solve: its certified sets
                 for (int k = gl; k < N; k += G) a.prev_sets[(size_t)k * a.nB + b] = HF(k);
                 for (int j = gl; j < NB; j += G) a.prev_sets[(size_t)(N + j) * a.nB + b] = BF(j);
+                if (gl == 0) a.prev_sets[(size_t)(N + NB) * a.nB + b] = a.prev_stamp;
             }
         }
     }
@@ -1658,7 +1660,7 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
                                  const int32_t *index, const int32_t *count, int32_t *retry,
                                  int32_t *retry_count, int pdas_cap, const uint32_t *warm,
                                  hipStream_t stream, unsigned long long *prof, bool f32, bool lti,
-                                 GroupDiag *diag, uint32_t *prev_sets) {
+                                 GroupDiag *diag, uint32_t *prev_sets, uint32_t prev_stamp) {
     if (capacity <= 0) return hipSuccess;
     if (!rmpc_mpc_group_supported(N, bs, no, f32) || (lti && bs != 1) || (f32 && lti)) return hipErrorInvalidValue;
     GroupArgs a;
@@ -1677,6 +1679,7 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
     a.chk = nullptr;
     a.site = nullptr;
     a.prev_sets = prev_sets;
+    a.prev_stamp = prev_stamp;
     const int G = group_lanes(N, bs), rpw = 64 / G;
     const int64_t need = (capacity + rpw - 1) / rpw;
     // RMPC_GROUP_PERSIST=<waves per CU> (diagnostics): capped grid looping over rounds

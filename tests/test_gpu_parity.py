@@ -856,7 +856,8 @@ def test_mpc_warm_start_closed_loop_same_optimum(rm, capsys):
       iterating go to the lane-group tail): same optimum;
     - a call of another batch size on the warm context starts cold (same iterations as cold
       under the same caps);
-    - an MPC rollout on a warm context reproduces the cold rollout (mpc_rate 1 and 5)."""
+    - an MPC rollout on a warm context reproduces the cold rollout (mpc_rate 1 and 5), and so
+      does a hybrid rollout (its MPC branch changes robots every step: per-robot stamps)."""
     from rmpc import workloads as W
     p3 = rm._native.mpc_params(20, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
     p4 = rm._native.mpc_params(30, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02,
@@ -903,6 +904,18 @@ def test_mpc_warm_start_closed_loop_same_optimum(rm, capsys):
             assert ro[True]["mpc_status"][0] == ro[False]["mpc_status"][0] > 0
             assert np.abs(ro[True]["states"] - ro[False]["states"]).max() <= 1e-9, rate
             assert np.abs(ro[True]["controls"] - ro[False]["controls"]).max() <= 1e-9, rate
+        # hybrid rollouts: the MPC branch (an index list that changes every step) warm-starts
+        # only the robots whose last solve was the previous step (per-robot stamps)
+        rp = rm._native.risk_params()
+        lp = rm._native.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0)
+        ro = {}
+        for on in (False, True):
+            rm.batch.set_warm_start(on, slot=3)
+            ro[on] = rm.batch.rollout_batch("hybrid", 80, lparams=lp, mparams=p3, rparams=rp, start_index=start,
+                                            obstacles=ompc.default_obstacles(), slot=3)
+        assert 0.05 < ro[True]["used_mpc"].mean() < 0.95
+        np.testing.assert_array_equal(ro[True]["used_mpc"], ro[False]["used_mpc"])
+        assert np.abs(ro[True]["states"] - ro[False]["states"]).max() <= 1e-9
     finally:
         rm.batch.set_warm_start(False, slot=3)
         rm.batch.set_stage_caps(0, 0, slot=3)
