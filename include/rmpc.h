@@ -164,12 +164,13 @@ int rmpc_ctx_set_side_stream(RmpcCtx *ctx, int32_t on);
  * with get_warm_start's shifted previous solution, mpc_controller.py:272-277, 470-475,
  * 524-538).  On, every whole-batch MPC call (rmpc_mpc_solve_batch[_dev]; MPC-mode rollouts)
  * starts robot b's active-set iteration from the sets certified by robot b's previous solve on
- * this context, shifted by one step (rollouts: by mpc_rate steps) with the last step repeated;
+ * this context, shifted by one step (MPC rollouts: by mpc_rate steps) with the last step repeated;
  * the context treats the robots of consecutive calls with the same (B, N, obstacle count,
  * formulation, precision) as the same controllers, and a call of another shape starts cold.
  * A performance setting like the reference's: the QP and its certified optimum do not change,
  * only the iteration count (`iters`).  Off (the default): every solve starts from empty sets.
- * Hybrid steps' MPC branch (index lists) always starts cold.  Turning it on resets the sets. */
+ * The hybrid step's MPC branch (a different robot subset each step) warm-starts only the robots
+ * whose previous solve was the previous call.  Turning it on resets the sets. */
 int rmpc_ctx_set_warm_start(RmpcCtx *ctx, int32_t on);
 int rmpc_mpc_stage_times(RmpcCtx *ctx, double *out3);
 
