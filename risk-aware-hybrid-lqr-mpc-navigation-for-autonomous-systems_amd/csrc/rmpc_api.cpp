@@ -605,13 +605,15 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             a.prev_stamp = ++c->warm_calls;
             // From warm sets most robots certify in their first or second solve, and a robot
             // still iterating after a few is one of the few hard ones: the tail's lane groups
-            // take it sooner.  fp64 LTV at N <= 20: 2 (config-3 closed loop, 65536 robots: 191M
-            // -> 274M solves/s, three fleets in flight 410M -> 498M); fp32 requests: 4 for the
-            // fp32 pass (config-4 closed loop, 32768 robots: 43.6M -> 64.2M, three fleets 61.6M
-            // -> 91.1M) (profiles/r03/closed_loop_warm.txt).  The caller's caps win.
+            // take it sooner.  fp64 LTV at N <= 20: 2 after a one-step shift (config-3 closed
+            // loop, 65536 robots: 191M -> 274M solves/s, three fleets in flight 410M -> 498M), 4
+            // after a longer one (mpc_rate 5: 178M -> 210M, three fleets 299M -> 315M; cap 2 there
+            // gave 169M / 248M); fp32 requests: 4 for the fp32 pass (config-4 closed loop, 32768
+            // robots: 43.6M -> 64.2M, three fleets 61.6M -> 91.1M)
+            // (profiles/r03/closed_loop_warm.txt).  The caller's caps win.
             if (!rmpc_knob("RMPC_FAST_CAP") && fast_cap <= 0 && c->fast_cap <= 0 && !lti) {
                 if (f32) a.pdas_cap = 4;
-                else if (p->horizon <= 20) a.pdas_cap = 2;
+                else if (p->horizon <= 20) a.pdas_cap = warm_shift == 1 ? 2 : 4;
             }
         }
         // RMPC_DENSE_PROF=1: per-phase cycle counters of the fast and dense kernels to

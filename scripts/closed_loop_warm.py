@@ -46,7 +46,10 @@ for f in range(max(SS)):
                        cnt=torch.zeros(4, dtype=torch.int64, device=dev),
                        stream=torch.cuda.Stream(device=dev), ctx=nat.context(0, 4 + f)))
 rp = nat.RolloutParams()
-rp.mode, rp.steps, rp.table_len, rp.mpc_rate, rp.plant_method = 1, K, 1000, 1, 0
+# CL_RATE: MPC every CL_RATE control steps (run_simulation.py's default is 5), zero-order hold
+# in between; the warm sets shift by CL_RATE steps.  Rates count MPC solves.
+rate = int(os.environ.get("CL_RATE", "1"))
+rp.mode, rp.steps, rp.table_len, rp.mpc_rate, rp.plant_method = 1, K, 1000, rate, 0
 rp.dt, rp.A, rp.a, rp.v_max, rp.omega_max = 0.02, 2.0, 0.5, 2.0, 3.0
 torch.cuda.synchronize()
 res = {}
@@ -77,7 +80,7 @@ for S in SS:
         res.setdefault((S, warm), fleets[0]["states"].cpu().numpy())
         _ = fleets[0]["states"].cpu().numpy()
         print(json.dumps({"fleets_in_flight": S, "warm_start": warm, "stage_caps": caps, "robots_per_fleet": B, "steps": K, "s": t,
-                          "mpc_solves_per_s": S * B * K / t, "ms_per_step": t / K * 1e3,
+                          "mpc_rate": rate, "mpc_solves_per_s": S * B * -(-K // rate) / t, "ms_per_step": t / K * 1e3,
                           "mpc_status_fleet0": fleets[0]["cnt"].cpu().tolist()}), flush=True)
     for fl in fleets:
         nat.check(lib.rmpc_ctx_set_warm_start(fl["ctx"], 0), "rmpc_ctx_set_warm_start")

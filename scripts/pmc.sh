@@ -9,7 +9,7 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU S
            "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM" \
            "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/${tag}_p$i -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${tag}_p$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/${tag}_p$i -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-closed-loop > gpurun_out/${tag}_p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc ($grp)"
   [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
 done

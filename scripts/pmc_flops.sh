@@ -4,11 +4,11 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 tag=${1:-flops}; shift
 timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 \
-  --output-format csv -d gpurun_out/${tag}_p1 -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-pcie "$@" \
+  --output-format csv -d gpurun_out/${tag}_p1 -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-pcie --no-closed-loop "$@" \
   > gpurun_out/${tag}_p1.log 2>&1
 rc=$?; echo "pass 1 rc=$rc"; [ $rc -ne 0 ] && exit $rc
 timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES \
-  --output-format csv -d gpurun_out/${tag}_p2 -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-pcie "$@" \
+  --output-format csv -d gpurun_out/${tag}_p2 -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-pcie --no-closed-loop "$@" \
   > gpurun_out/${tag}_p2.log 2>&1
 rc=$?; echo "pass 2 rc=$rc"; [ $rc -ne 0 ] && exit $rc
 python3 scripts/pmc_flops.py gpurun_out/${tag} gpurun_out/${tag}_flops.json

@@ -5,7 +5,7 @@ tag=${1:-hbm}
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -s KILL 150 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/${tag}_p$i -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/${tag}_p$i.log 2>&1
+  timeout -s KILL 150 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/${tag}_p$i -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-closed-loop > gpurun_out/${tag}_p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc ($grp)"
   [ $rc -ne 0 ] && exit $rc
 done
