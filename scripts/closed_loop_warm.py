@@ -7,7 +7,7 @@ its own context and stream (one fleet's closed loop cannot overlap its own steps
 fleets can, as bench.py's batches in flight).  Prints one JSON line per (S, warm) and the largest
 state difference between the warm and cold closed loops.
 Usage: python scripts/closed_loop_warm.py [B] [steps] [S ...]   (CL_CAPS="f,t;f,t..." also times
-the warm loop under other stage caps, rmpc_ctx_set_stage_caps)"""
+the warm loop under other stage caps, rmpc_ctx_set_stage_caps; CL_COLD_CAPS the cold one)"""
 import ctypes as C
 import json
 import os
@@ -54,6 +54,7 @@ rp.dt, rp.A, rp.a, rp.v_max, rp.omega_max = 0.02, 2.0, 0.5, 2.0, 3.0
 torch.cuda.synchronize()
 res = {}
 runs = [(False, "0,0"), (True, "0,0")] + [(True, c) for c in os.environ.get("CL_CAPS", "").split(";") if c]
+runs += [(False, c) for c in os.environ.get("CL_COLD_CAPS", "").split(";") if c]   # cold under other caps
 for S in SS:
     for warm, caps in runs:
         for fl in fleets[:S]:
