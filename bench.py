@@ -83,6 +83,220 @@ def algorithmic_bytes(N, n_obs, n_out_rows=True):
     return inb + outb
 
 
+# ---- multi-rank plumbing: one process per GPU ----------------------------------
+
+def rank_env(args):
+    """(world, rank, local rank) of this process.  Under a launcher (torchrun, or spawn_ranks
+    below) WORLD_SIZE is set and must equal --gpus; without one, --gpus 1 is the single
+    process and --gpus N > 1 returns world None: the caller starts the N ranks itself."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus > 1:
+            return None, 0, 0
+        return 1, 0, 0
+    world = int(env_world)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU "
+                         "with --gpus equal to the launcher's process count")
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def spawn_ranks(n, argv, grace_s=30.0):
+    """`python bench.py --gpus N` with no launcher: start N child processes of this script, one
+    per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (127.0.0.1
+    unless MASTER_ADDR is given).  This parent never imports torch or touches a GPU, and never
+    execs: the children are new processes (subprocess.Popen).  Each child dies with the parent
+    (PR_SET_PDEATHSIG).  If any child fails or is killed the others are terminated and the
+    parent exits non-zero; otherwise it relays rank 0's one JSON line (checking n_gpus == N)."""
+    import signal
+    import socket
+    import subprocess
+    import tempfile
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        free_port = s.getsockname()[1]
+    addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = os.environ.get("MASTER_PORT", str(free_port))
+
+    def die_with_parent():                 # runs in the child between fork and exec
+        import ctypes
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)   # PR_SET_PDEATHSIG
+
+    out0 = tempfile.TemporaryFile(mode="w+")
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR=addr, MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=out0 if r == 0 else sys.stderr, preexec_fn=die_with_parent))
+
+    def stop_all(*_):
+        for q in procs:
+            if q.poll() is None:
+                q.terminate()
+        t_end = time.time() + grace_s
+        for q in procs:
+            try:
+                q.wait(max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                q.kill()
+                q.wait()
+    old = {sig: signal.signal(sig, lambda s_, f_: (stop_all(), sys.exit(128 + s_))) for sig in (signal.SIGTERM, signal.SIGINT)}
+    failed = None
+    while failed is None and any(q.poll() is None for q in procs):
+        for r, q in enumerate(procs):
+            if q.poll() not in (None, 0):
+                failed = (r, q.returncode)
+                break
+        time.sleep(0.1)
+    if failed is None:
+        failed = next(((r, q.returncode) for r, q in enumerate(procs) if q.returncode != 0), None)
+    if failed is not None:
+        stop_all()
+    for sig, h in old.items():
+        signal.signal(sig, h)
+    if failed is not None:
+        print(f"bench.py: rank {failed[0]} of {n} exited with status {failed[1]}", file=sys.stderr)
+        return failed[1] if failed[1] > 0 else 128 - failed[1]
+    out0.seek(0)
+    lines = [ln for ln in out0.read().splitlines() if ln.startswith("{")]
+    if len(lines) != 1:
+        print(f"bench.py: rank 0 printed {len(lines)} JSON lines, expected 1", file=sys.stderr)
+        return 1
+    if json.loads(lines[0]).get("n_gpus") != n:
+        print(f"bench.py: rank 0 reports n_gpus != {n}", file=sys.stderr)
+        return 1
+    print(lines[0], flush=True)
+    return 0
+
+
+def init_dist(args, world, local):
+    """The process group of an N > 1 run: RCCL ("nccl", one GPU per rank, bound to cuda:local),
+    or gloo for --rehearse-one-gpu / --selftest.  None for a single process."""
+    if world == 1:
+        return None
+    import torch
+    import torch.distributed as dist
+    if args.selftest or args.rehearse_one_gpu:
+        dist.init_process_group("gloo")
+    else:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+    return dist
+
+
+def coll_device(args, dev):
+    """Where collective tensors live: the rank's GPU for RCCL, the host for gloo."""
+    import torch
+    return torch.device("cpu") if (args.selftest or args.rehearse_one_gpu) else dev
+
+
+def parallelism(args, world):
+    s = f"batch-split x{world} (no data-path collective)"
+    if args.rehearse_one_gpu and world > 1:
+        s += "; rehearsal: every rank on cuda:0, gloo collectives (not a scaling number)"
+    return s
+
+
+def timed_loop(step, steps, warmup, dist, sync, S=1):
+    """The timing contract: max(W, S) untimed steps, then exactly K steps (step k on in-flight
+    slot k mod S) bracketed by barrier + synchronize on both sides.  Returns this rank's
+    elapsed seconds (the caller takes the MAX over ranks)."""
+    sync()
+    for k in range(max(warmup, S)):
+        step(k)
+    sync()
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(k)
+    sync()
+    if dist:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def gather_loop(step, local_u0, dist, world, rank, steps, sync, cdev):
+    """N > 1: K more steps with SURVEY 8(e)'s batch gather inside the timed region -- after
+    every step the rank's u0 shard is all-gathered and interleaved back into global robot order
+    (rmpc.workloads.gather_interleaved; RCCL over xGMI, or gloo through the host).  Returns
+    (slowest rank's elapsed s, the last gathered u0 [world * B, 2] on cdev)."""
+    from rmpc import workloads as W
+    g_out = None
+
+    def step_gather():
+        nonlocal g_out
+        step()
+        g, g_out = W.gather_interleaved(dist, local_u0().to(cdev), world, g_out)
+        return g
+    step_gather()
+    sync()
+    dist.barrier()
+    sync()
+    t = time.perf_counter()
+    for _ in range(steps):
+        g = step_gather()
+    sync()
+    dist.barrier()
+    elapsed = time.perf_counter() - t
+    assert bool((g[rank::world] == local_u0().to(cdev)).all())
+    elapsed, _ = W.aggregate(dist, elapsed, [], device=cdev)
+    return elapsed, g
+
+
+def selftest_rank(args, world, rank):
+    """--selftest: one rank of the multi-rank flow on the CPU (gloo), with the oracle's C port
+    standing in for the device solve (a checker of the launcher and collectives, never a
+    measurement): its round-robin shard of a config-3 batch, the setup broadcast, the timed
+    loop, the gathered leg and the MAX / SUM aggregation -- the same functions as the GPU run.
+    Rank 0 prints one JSON line (and saves the gathered u0 with --selftest-out)."""
+    import numpy as np
+    import torch
+    from oracle import cpu, figure8
+    from rmpc import workloads as W
+
+    dist = init_dist(args, world, 0)
+    if rank == args.selftest_fail_rank:
+        sys.exit(3)                        # the others now block in their first collective
+    cfg = W.CONFIGS["cfg3"]
+    N, B_total = cfg["N"], args.selftest_batch * world
+    idx = W.shard_indices(B_total, world, rank)
+    xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, W.t0_at(idx, B_total), N + 1)
+    x0 = xr[:, 0] + W.noise_at(idx, cfg["seed"])
+    obs = torch.tensor(cfg["obs"], dtype=torch.float64) if rank == 0 else torch.zeros(len(cfg["obs"]), 3, dtype=torch.float64)
+    obs = W.broadcast_shared(dist, obs)
+    p = cpu.mpc_params(N, (15, 15, 50), (.1, .1), (30, 30, 40), 0.3, 5000., 2., 3., 0.02)
+    res = {}
+
+    def step(k=0):
+        res["out"] = cpu.mpc_solve_batch(p, x0, xr, ur, obs.numpy(), step_count=np.full(idx.size, 10, np.int32))
+    nosync = lambda: None                                      # noqa: E731
+    elapsed = timed_loop(step, args.steps, args.warmup, dist, nosync)
+    u0 = lambda: torch.from_numpy(res["out"]["u0"])            # noqa: E731
+    elapsed_g, g = (None, u0()) if dist is None else gather_loop(step, u0, dist, world, rank, args.steps,
+                                                                 nosync, torch.device("cpu"))
+    st = res["out"]["status"]
+    elapsed, counts = W.aggregate(dist, elapsed, [int((st == c).sum()) for c in (0, 1, 2)])
+    line = {"metric": "SELFTEST (C port on the CPU, not a measurement): MPC QP solves/sec", "selftest": True,
+            "value": B_total * args.steps / elapsed, "unit": "solves/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"cfg3 shape, {args.selftest_batch} robots/rank", "global_batch": B_total,
+                       "parallelism": f"batch-split x{world}, gloo"},
+            "solver": dict(optimal=counts[0], inaccurate=counts[1], fallback=counts[2])}
+    if elapsed_g is not None:
+        line["value_with_gather"] = B_total * args.steps / elapsed_g
+    if rank == 0:
+        if args.selftest_out:
+            np.save(args.selftest_out, g.numpy())
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -109,11 +323,23 @@ def main():
     ap.add_argument("--inflight", type=int, default=3,
                     help="MPC configs: batches in flight at once, each on its own stream with its own "
                          "solver context and outputs (step k runs on stream k mod S)")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="N>1 on a one-GPU box: every rank on cuda:0, gloo collectives through host "
+                         "tensors (exercises the multi-rank bench flow; not a scaling number)")
+    ap.add_argument("--selftest", action="store_true",
+                    help="CPU-only self-test of the multi-rank flow (gloo, the C port in place of the "
+                         "device solve): launcher, timing collectives and the batch gather")
+    ap.add_argument("--selftest-batch", type=int, default=1024, help="--selftest: robots per rank")
+    ap.add_argument("--selftest-out", default=None, help="--selftest: rank 0 saves the gathered u0 here (.npy)")
+    ap.add_argument("--selftest-fail-rank", type=int, default=-1,
+                    help="--selftest: this rank exits with status 3 after joining the group (launcher test)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = rank_env(args)
+    if world is None:                     # --gpus N > 1 without a launcher: start the N ranks
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    if args.selftest:
+        return selftest_rank(args, world, rank)
     # config 2's SciPy leg forks its worker pool, so it runs before the GPU is initialised
     pre = None
     if args.config == "cfg2" and world == 1 and not args.no_cpu_baseline:
@@ -121,11 +347,10 @@ def main():
     import numpy as np
     import torch
 
+    if args.rehearse_one_gpu:
+        local = 0
     torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dist = init_dist(args, world, local)
 
     import rmpc
     from rmpc import workloads as W
@@ -158,7 +383,8 @@ def main():
     x0_h, xr_h, ur_h = fleets[0]["x0_h"], fleets[0]["xr_h"], fleets[0]["ur_h"]
     x0, xr, ur = fleets[0]["x0"], fleets[0]["xr"], fleets[0]["ur"]
     obs = torch.tensor(obs_list, dtype=torch.float64, device=dev).reshape(-1, 3)
-    W.broadcast_shared(dist, obs)          # rank 0's obstacles on every rank (setup, untimed)
+    cdev = coll_device(args, dev)          # collectives: the GPU (RCCL) or, for gloo, the host
+    obs = W.broadcast_shared(dist, obs.to(cdev)).to(dev)   # rank 0's obstacles on every rank (setup, untimed)
 
     def new_out():
         return dict(u0=torch.empty(B, 2, dtype=torch.float64, device=dev),
@@ -204,21 +430,7 @@ def main():
 
     # inputs, outputs and step counters were written on the default stream: the other
     # streams start only after that work (they are non-blocking streams)
-    torch.cuda.synchronize()
-    for k in range(max(args.warmup, S)):
-        step(k)
-    torch.cuda.synchronize()
-
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for k in range(args.steps):
-        step(k)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
+    elapsed = timed_loop(step, args.steps, args.warmup, dist, torch.cuda.synchronize, S)
     # one batch's launch on its own (HIP events on the launch stream, no other batch in
     # flight): the roofline's kernel time
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -264,31 +476,14 @@ def main():
     # back into global robot order by a transpose of the [world][B] result)
     elapsed_g = None
     if dist:
-        g_out = torch.empty(world * B, 2, dtype=torch.float64, device=dev)
-
-        def step_gather():
-            step()
-            return W.gather_interleaved(dist, out["u0"], world, g_out)[0]
-        step_gather()
-        torch.cuda.synchronize()
-        dist.barrier()
-        torch.cuda.synchronize()
-        t_g = time.perf_counter()
-        for _ in range(args.steps):
-            u0_global = step_gather()
-        torch.cuda.synchronize()
-        dist.barrier()
-        elapsed_g = time.perf_counter() - t_g
-        assert torch.equal(u0_global[rank::world], out["u0"])
-        tt = torch.tensor([elapsed_g], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed_g = float(tt.item())
+        elapsed_g, u0_global = gather_loop(step, lambda: out["u0"], dist, world, rank, args.steps,
+                                           torch.cuda.synchronize, cdev)
 
     st = out["status"].cpu().numpy()
     its = out["iters"].cpu().numpy()
     counts = [int((st == 0).sum()), int((st == 1).sum()), int((st == 2).sum())]
     # the only collectives: MAX of the elapsed time, SUM of the status counts
-    elapsed, counts = W.aggregate(dist, elapsed, counts, device=dev)
+    elapsed, counts = W.aggregate(dist, elapsed, counts, device=cdev)
     stats = dict(optimal=counts[0], inaccurate=counts[1], fallback=counts[2],
                  iters_mean=round(float(its.mean()), 3),
                  iters_p99=float(np.percentile(its, 99)), iters_max=int(its.max()),
@@ -331,7 +526,7 @@ def main():
         "config": {"workload": f"{args.config}: {'solve (LTI)' if args.lti else 'solve_with_ltv'}, N={N}, {n_obs} obstacles, "
                                f"Q=[15,15,50] R=[.1,.1] P=[30,30,40] rho=5000, {B_per} robots/GPU",
                    "robots_per_gpu": B_per, "global_batch": B_total, "horizon": N,
-                   "n_obstacles": n_obs, "parallelism": f"batch-split x{world} (no collective)",
+                   "n_obstacles": n_obs, "parallelism": parallelism(args, world),
                    "batches_in_flight": S, "stage_caps": list(caps) if caps[0] else "library default"},
         # compute-bound path on the vector ALU (MFMA unused by the default pipeline): priced at
         # the FP64 (FP32 for config 4) vector peak.  `achieved`/`frac` use SURVEY 8(d)'s
@@ -557,20 +752,7 @@ def _timed(args, step, dist, dev, S=1):
     own device time).  Returns (elapsed s, event ms list)."""
     import torch
     stream = torch.cuda.current_stream()
-    torch.cuda.synchronize()       # per-slot state written on the default stream comes first
-    for k in range(max(args.warmup, S)):
-        step(k)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_loop(step, args.steps, args.warmup, dist, torch.cuda.synchronize, S)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
     for i in range(args.steps):
@@ -735,10 +917,7 @@ def bench_other(args, world, rank, local, dist, pre=None):
         torch.cuda.synchronize()
         alone_default_s = float(np.mean([a.elapsed_time(b) for a, b in ev2[2:]])) / 1e3
         rmpc.batch.set_stage_caps(*caps, device=local, slot=0)
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed, _ = W.aggregate(dist, elapsed, [], device=coll_device(args, dev))
     line = {"metric": metric, "value": B_total * args.steps / elapsed,
             "value_one_batch_alone": B_total / k_avg_s, "unit": unit, "n_gpus": world,
             **({"value_one_batch_alone_default_caps": B_total / alone_default_s} if alone_default_s else {}),
@@ -746,7 +925,7 @@ def bench_other(args, world, rank, local, dist, pre=None):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: Figure-8 references at per-robot time offsets + seeded start noise",
             "config": {"workload": workload, "robots_per_gpu": B_per, "global_batch": B_total,
-                       "parallelism": f"batch-split x{world} (no collective)", "batches_in_flight": S}}
+                       "parallelism": parallelism(args, world), "batches_in_flight": S}}
     if args.config == "cfg5":
         line["config"]["stage_caps"] = list(caps) if caps[0] else "library default"
     if flops_unit:

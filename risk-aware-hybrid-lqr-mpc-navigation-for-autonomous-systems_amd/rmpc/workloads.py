@@ -136,6 +136,8 @@ def aggregate(dist, elapsed, counts, device="cpu"):
     import torch
     tt = torch.tensor([float(elapsed)], dtype=torch.float64, device=device)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    if not len(counts):
+        return float(tt.item()), []
     cc = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=device)
     dist.all_reduce(cc)
     return float(tt.item()), [int(v) for v in cc.tolist()]

@@ -164,3 +164,65 @@ def test_gloo_two_ranks_split_solve_gather_matches_single_process():
     ref = cpu.mpc_solve_batch(p, x0, xr, ur, W.DEFAULT_OBS, step_count=np.full(B_total, 10, np.int32))
     for _, u0_global in res:
         np.testing.assert_array_equal(u0_global, ref["u0"])
+
+
+def _bench(args, env=None, timeout=240):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=e, cwd="/tmp",
+                          capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.timeout(300)
+def test_bench_launcher_spawns_ranks_and_gathers(tmp_path):
+    """`python bench.py --gpus 2` with no launcher starts its own two ranks (bench.spawn_ranks:
+    child processes with RANK / WORLD_SIZE / MASTER_*), here through the CPU self-test mode
+    (gloo, the C port in place of the device solve; the same timing loop, aggregate and
+    gather_interleaved as the GPU run).  Exactly one JSON line comes back, with n_gpus 2 and the
+    gathered leg; the gathered u0 is bit-identical to one process solving the whole batch."""
+    import json
+    from oracle import cpu, figure8
+    out = tmp_path / "u0.npy"
+    r = _bench(["--gpus", "2", "--selftest", "--selftest-batch", "512", "--steps", "2", "--warmup", "1",
+                "--selftest-out", str(out)])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["selftest"] is True
+    assert line["value"] > 0 and line["value_with_gather"] > 0
+    assert line["config"]["global_batch"] == 1024 and line["solver"]["optimal"] == 1024
+    B_total, N = 1024, 20
+    idx = np.arange(B_total)
+    xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, W.t0_at(idx, B_total), N + 1)
+    x0 = xr[:, 0] + W.noise_at(idx, W.CONFIGS["cfg3"]["seed"])
+    p = cpu.mpc_params(N, (15, 15, 50), (.1, .1), (30, 30, 40), 0.3, 5000., 2., 3., 0.02)
+    ref = cpu.mpc_solve_batch(p, x0, xr, ur, W.DEFAULT_OBS, step_count=np.full(B_total, 10, np.int32))
+    np.testing.assert_array_equal(np.load(out), ref["u0"])
+
+
+@pytest.mark.timeout(300)
+def test_bench_launcher_fails_when_a_rank_fails():
+    """A rank that dies (status 3 after joining the group, while its peer waits in a
+    collective) ends the whole job: the parent terminates the other rank, prints no JSON line and
+    exits non-zero, well before any collective timeout."""
+    import time
+    t = time.time()
+    r = _bench(["--gpus", "2", "--selftest", "--selftest-batch", "64", "--steps", "1", "--warmup", "0",
+                "--selftest-fail-rank", "1"])
+    assert r.returncode != 0
+    assert "rank 1 of 2 exited with status 3" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert time.time() - t < 120
+
+
+def test_bench_world_size_must_match_gpus():
+    """Under a launcher, WORLD_SIZE and --gpus must agree (a torchrun of 2 ranks with --gpus 1
+    would otherwise report the wrong n_gpus)."""
+    r = _bench(["--gpus", "1", "--selftest"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=2 but --gpus 1" in r.stderr
