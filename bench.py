@@ -490,12 +490,9 @@ def main():
                  slack_active_frac=round(float(out["slack_used"].float().mean().item()), 4))
 
     n_obs = len(obs_list)
-    dense_tail = os.environ.get("RMPC_TAIL", "") == "dense"
     fast_name = "mpc_ltv_fast_kernel"
-    tail_name = "mpc_dense_kernel" if dense_tail else "mpc_group_kernel"
-    pipe = ("fp64 VALU lane-per-robot stage + " +
-            ("wave-per-robot MFMA f64 (v_mfma_f64_16x16x4) condensed tail" if dense_tail
-             else "lane-group VALU Riccati tail (MFMA unused)"))
+    tail_name = "mpc_group_kernel"
+    pipe = "fp64 VALU lane-per-robot stage + lane-group VALU Riccati tail (MFMA unused)"
     if f32:
         pipe = pipe.replace("fp64 VALU lane-per-robot stage",
                             "fp32 VALU lane-per-robot stage (active sets) + fp64 refinement pass of the same kernel")

@@ -115,6 +115,13 @@ struct RmpcCtx {
     // the robots it hands on go to a list of their own (retry_r, sets retry_sets_r)
     hipEvent_t rev[2] = {nullptr, nullptr};
     DevBuf retry_r, retry_sets_r;
+    // Consecutive calls share state on the device (list counters zeroed by the previous
+    // pipeline, the hybrid step's counter pairs, warm-start sets and stamps), which is correct
+    // in stream order.  A call on another stream than the previous call's first waits for that
+    // call (order_calls): an event recorded at the end of every stateful call (last_ev).
+    hipEvent_t last_ev = nullptr;
+    hipStream_t last_s = nullptr;
+    bool last_valid = false;
     std::mutex mu;
     // multi-device context (rmpc_ctx_create_multi): one single-device context per entry;
     // empty for a single-device context
@@ -274,6 +281,7 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
         if (e) (void)hipEventDestroy(e);
     for (auto &e : c->rev)
         if (e) (void)hipEventDestroy(e);
+    if (c->last_ev) (void)hipEventDestroy(c->last_ev);
     c->retry_r.release();
     c->retry_sets_r.release();
     c->retry2.release();
@@ -448,6 +456,23 @@ static hipError_t side_stream(RmpcCtx *c) {
     return e;
 }
 
+// Stream order between consecutive stateful calls of one context (RmpcCtx::last_ev): a call
+// on another stream than the previous one waits for the previous call's end on the device.
+static hipError_t order_calls(RmpcCtx *c, hipStream_t s) {
+    if (c->last_valid && c->last_s != s) return hipStreamWaitEvent(s, c->last_ev, 0);
+    return hipSuccess;
+}
+static hipError_t mark_call(RmpcCtx *c, hipStream_t s) {
+    if (!c->last_ev) {
+        const hipError_t e = hipEventCreateWithFlags(&c->last_ev, hipEventDisableTiming);
+        if (e != hipSuccess) { c->last_ev = nullptr; return e; }
+    }
+    const hipError_t e = hipEventRecord(c->last_ev, s);
+    c->last_valid = e == hipSuccess;
+    c->last_s = s;
+    return e;
+}
+
 // The context's own stream (host-pointer entry points), created on first use; NULL (the null
 // stream) if creation fails
 static hipStream_t own(RmpcCtx *c) {
@@ -491,10 +516,10 @@ static void flip_counts(RmpcCtx *c) {
 
 // Launch the MPC solve for B robots (or the robots of a device-side index list): the
 // register-resident lane-per-robot kernel when (N, block size) is instantiated; the robots
-// it does not certify within its PDAS cap go to the wave-per-robot dense kernel, and what
+// it does not certify within its PDAS cap go to the lane-group tail, and what
 // that one hands on (non-finite data -> fallback law, uncertified) to the generic kernel.
 // Otherwise the generic kernel alone.
-static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const double *x0,
+static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const double *x0,
                       const double *x_refs, int32_t ref_rows, const double *u_refs, int32_t uref_rows,
                       const double *obstacles, int32_t n_obs, int32_t *step_count, double *u0,
                       double *u_seq, double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
@@ -506,10 +531,19 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
     MpcDevParams d = to_dev(p);
     const bool lti = p->formulation == RMPC_LTI;
     d.ref_off = ref_off;
-    const bool f32 = p->precision == RMPC_F32;
     // hard half-spaces (soft = 0 with obstacles): augmented-Lagrangian rounds in the generic kernel
     const bool hard = !p->soft && n_obs > 0;
-    const bool fast = !hard && rmpc_mpc_fast_supported(p->horizon, bs, p->precision, p->formulation == RMPC_LTI, n_obs) &&
+    // An fp32 request (BASELINE config 4) computes in fp32 only where an fp64 pass re-solves and
+    // re-certifies the fp32 pass's active sets: the soft LTV lane-per-robot instances with a
+    // refinement pass (N = 20, and N = 30 with 8 obstacles).  Every other fp32 request runs the
+    // fp64 pipeline, so every control an fp32 request returns is the fp64 optimum.
+    // (RMPC_NO_REFINE=1, diagnostics: fp32 arithmetic wherever an fp32 kernel exists, outputs
+    // fp32-rounded -- the round-2 behaviour)
+    const bool no_refine = rmpc_knob("RMPC_NO_REFINE") != nullptr;
+    const bool f32 = p->precision == RMPC_F32 &&
+                     (no_refine || (!lti && !hard && rmpc_mpc_refine_supported(p->horizon, bs, n_obs)));
+    const int prec = f32 ? RMPC_F32 : RMPC_F64;
+    const bool fast = !hard && rmpc_mpc_fast_supported(p->horizon, bs, prec, lti, n_obs) &&
                       !rmpc_knob("RMPC_DISABLE_FAST");
     // fp64 without a lane-per-robot instance -- LTI (MPCController.solve, mpc_node's path),
     // or an LTV (N, block size) the fast kernel is not built for (N = 30) -- every robot
@@ -611,12 +645,14 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             // gave 169M / 248M); fp32 requests: 4 for the fp32 pass (config-4 closed loop, 32768
             // robots: 43.6M -> 64.2M, three fleets 61.6M -> 91.1M)
             // (profiles/r03/closed_loop_warm.txt).  The caller's caps win.
-            if (!rmpc_knob("RMPC_FAST_CAP") && fast_cap <= 0 && c->fast_cap <= 0 && !lti) {
+            // (Not on the first call after a reset, whose sets are all zero: a cold start, which
+            // keeps the cold default.)
+            if (!rmpc_knob("RMPC_FAST_CAP") && fast_cap <= 0 && c->fast_cap <= 0 && !lti && c->warm_calls > 1) {
                 if (f32) a.pdas_cap = 4;
                 else if (p->horizon <= 20) a.pdas_cap = warm_shift == 1 ? 2 : 4;
             }
         }
-        // RMPC_DENSE_PROF=1: per-phase cycle counters of the fast and dense kernels to
+        // RMPC_DENSE_PROF=1: per-phase cycle counters of the fast and lane-group kernels to
         // stderr (synchronises the stream; diagnostics only)
         const bool prof = rmpc_knob("RMPC_DENSE_PROF") != nullptr;
         unsigned long long *pc = nullptr;
@@ -652,8 +688,7 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         // `extra_cap` solves); it writes the outputs, which are therefore fp64-exact.  What it
         // does not certify joins the fp64 tail's list.  (RMPC_NO_REFINE=1: the fp32 pass writes
         // its own outputs, the round-2 behaviour; A/B only)
-        const bool refine = f32 && warm && rmpc_mpc_refine_supported(p->horizon, bs, n_obs) &&
-                            !rmpc_knob("RMPC_NO_REFINE");
+        const bool refine = f32 && warm && rmpc_mpc_refine_supported(p->horizon, bs, n_obs) && !no_refine;
         if (refine) {
             HIP_TRY(c->refine.ensure((size_t)B * sizeof(int32_t)));
             HIP_TRY(c->refine_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
@@ -673,26 +708,49 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
                 ai.retry = (int32_t *)lists[i % 2]->p;
                 ai.retry_count = pass_cnt[i];
                 ai.retry_sets = (uint32_t *)sets[i % 2]->p;
-                HIP_TRY(rmpc_launch_mpc_fast(ai, p->horizon, bs, p->precision, s, lti));
+                HIP_TRY(rmpc_launch_mpc_fast(ai, p->horizon, bs, prec, s, lti));
                 dbg_sync(s, "fast pass");
                 a.index = ai.retry;        // the next pass: that list, from its sets
                 a.count = ai.retry_count;
                 a.warm_sets = ai.retry_sets;
             }
         }
-        HIP_TRY(rmpc_launch_mpc_fast(a, p->horizon, bs, p->precision, s, lti));
-        // tail: the lane-group Riccati kernel (default) or the condensed wave-per-robot one
-        // (RMPC_TAIL=dense); RMPC_DISABLE_DENSE skips the tail stage altogether
-        const char *tail = rmpc_knob("RMPC_TAIL");
-        const bool use_dense = tail && !strcmp(tail, "dense") && !lti &&   // the dense tail is LTV-only
-                               rmpc_mpc_dense_supported(p->horizon, bs, n_obs);   // (and built: make DENSE=1)
-        const bool group_tail = !use_dense && rmpc_mpc_group_supported(p->horizon, bs, n_obs) &&
-                                !rmpc_knob("RMPC_DISABLE_DENSE");
+        HIP_TRY(rmpc_launch_mpc_fast(a, p->horizon, bs, prec, s, lti));
+        // tail: the lane-group Riccati kernel (RMPC_DISABLE_DENSE: no tail stage, A/B only)
+        const bool group_tail = rmpc_mpc_group_supported(p->horizon, bs, n_obs) && !rmpc_knob("RMPC_DISABLE_DENSE");
         // The refinement and the tail work on disjoint robots (the fp32 pass's certified ones
         // and the rest): the refinement runs on the side stream while the tail runs here, and
         // the robots it hands on get a second, short tail launch after the join
         // (RMPC_REFINE_INLINE=1: refinement, then one tail, on this stream; A/B)
         const bool refine_side = refine && group_tail && c->use_side && !rmpc_knob("RMPC_REFINE_INLINE");
+        // Everything the side branch and the tails use is allocated before the fork, and every
+        // error after the fork joins the side branch first (`join`): the call's stream must
+        // never complete ahead of a refinement kernel that is still writing outputs.
+        if (group_tail) HIP_TRY(c->retry2.ensure((size_t)B * sizeof(int32_t)));
+        if (refine_side) {
+            HIP_TRY(side_stream(c));
+            for (auto &e : c->rev)
+                if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            HIP_TRY(c->retry_r.ensure((size_t)B * sizeof(int32_t)));
+            HIP_TRY(c->retry_sets_r.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
+        }
+        bool forked = false;
+        auto join = [&]() -> hipError_t {    // side branch -> call's stream (host sync as a last resort)
+            if (!forked) return hipSuccess;
+            forked = false;
+            hipError_t e = hipEventRecord(c->rev[1], c->side);
+            if (e == hipSuccess) e = hipStreamWaitEvent(s, c->rev[1], 0);
+            if (e != hipSuccess) (void)hipStreamSynchronize(c->side);
+            return e;
+        };
+#define HIP_TRY_J(expr)                      \
+    do {                                     \
+        const hipError_t ej_ = (expr);       \
+        if (ej_ != hipSuccess) {             \
+            (void)join();                    \
+            HIP_TRY(ej_);                    \
+        }                                    \
+    } while (0)
         if (refine) {
             dbg_sync(s, "fast (fp32 sets)");
             MpcFastArgs r = a;
@@ -707,22 +765,17 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             r.prof = pc ? pc + 64 : nullptr;   // (diagnostics: the refinement pass's own counters)
             hipStream_t rs = s;
             if (refine_side) {
-                HIP_TRY(side_stream(c));
-                for (auto &e : c->rev)
-                    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-                HIP_TRY(c->retry_r.ensure((size_t)B * sizeof(int32_t)));
-                HIP_TRY(c->retry_sets_r.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
                 r.retry = (int32_t *)c->retry_r.p;
                 r.retry_count = cnt + 10;
                 r.retry_sets = (uint32_t *)c->retry_sets_r.p;
                 HIP_TRY(hipEventRecord(c->rev[0], s));
                 HIP_TRY(hipStreamWaitEvent(c->side, c->rev[0], 0));
+                forked = true;
                 rs = c->side;
             }
-            HIP_TRY(rmpc_launch_mpc_fast(r, p->horizon, bs, RMPC_F64, rs, lti));
-            if (refine_side) HIP_TRY(hipEventRecord(c->rev[1], c->side));
+            HIP_TRY_J(rmpc_launch_mpc_fast(r, p->horizon, bs, RMPC_F64, rs, lti));
         }
-        if (c->timing) HIP_TRY(hipEventRecord(c->ev[1], s));
+        if (c->timing) HIP_TRY_J(hipEventRecord(c->ev[1], s));
         dbg_sync(s, "fast");
         const int32_t *left = (const int32_t *)c->retry.p;
         const int32_t *left_n = cnt;
@@ -730,20 +783,18 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
         const int tail_cap = rmpc_knob("RMPC_DENSE_CAP") ? atoi(rmpc_knob("RMPC_DENSE_CAP"))
                              : c->tail_cap > 0          ? c->tail_cap
                                                         : (p->horizon <= 20 ? 4 : 6);
-        // fp32 requests get the fp32 lane-group tail (RMPC_TAIL64=1: the fp64 one)
-        const bool tail32 = f32 && !rmpc_knob("RMPC_TAIL64") && rmpc_mpc_group_supported(p->horizon, bs, n_obs, true);
+        // a refined fp32 request always takes the fp64 tail (it returns fp64 optima only); the
+        // fp32 lane-group tail is a diagnostics variant (RMPC_TAIL32=1 with RMPC_NO_REFINE=1)
+        const bool tail32 = f32 && !refine && !rmpc_knob("RMPC_TAIL64") &&
+                            rmpc_mpc_group_supported(p->horizon, bs, n_obs, true);
         if (group_tail) {
-            HIP_TRY(c->retry2.ensure((size_t)B * sizeof(int32_t)));
             int32_t *cnt2 = cnt + 8;
-            const hipError_t ea = rmpc_launch_mpc_group(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs,
-                                                        uref_rows, obstacles, step_count, u0, u_seq, x_pred, cost,
-                                                        status, slack_used, iters, left, left_n,
-                                                        (int32_t *)c->retry2.p, cnt2, tail_cap, a.retry_sets, s, pc,
-                                                        tail32, lti, &c->gdiag, a.prev_sets, a.prev_stamp);
-            // join the refinement before anything else, also when the tail's launch failed (the
-            // call's stream must not complete ahead of the side branch)
-            if (refine_side) HIP_TRY(hipStreamWaitEvent(s, c->rev[1], 0));
-            HIP_TRY(ea);
+            HIP_TRY_J(rmpc_launch_mpc_group(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs, uref_rows,
+                                            obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
+                                            iters, left, left_n, (int32_t *)c->retry2.p, cnt2, tail_cap,
+                                            a.retry_sets, s, pc, tail32, lti, &c->gdiag, a.prev_sets, a.prev_stamp));
+            HIP_TRY(join());               // the refinement, before anything else on this stream
+#undef HIP_TRY_J
             if (refine_side) {            // the refinement's hand-ons (same output list)
                 HIP_TRY(rmpc_launch_mpc_group(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs, uref_rows,
                                               obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
@@ -790,47 +841,10 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
             dbg_sync(s, "group");
             left = (const int32_t *)c->retry2.p;
             left_n = cnt2;
-        } else if (!lti && rmpc_mpc_dense_supported(p->horizon, bs, n_obs) && !rmpc_knob("RMPC_DISABLE_DENSE")) {
-            HIP_TRY(c->retry2.ensure((size_t)B * sizeof(int32_t)));
-            int32_t *cnt2 = cnt + 8;
-            HIP_TRY(rmpc_launch_mpc_dense_f64(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs,
-                                              uref_rows, obstacles, step_count, u0, u_seq, x_pred, cost,
-                                              status, slack_used, iters, left, left_n,
-                                              (int32_t *)c->retry2.p, cnt2, cnt + 12,
-                                              tail_cap,
-                                              a.retry_sets, s, pc));
-            if (prof) {
-                unsigned long long h[64];
-                int32_t cn[16];
-                HIP_TRY(hipMemcpyAsync(h, pc, sizeof(h), hipMemcpyDeviceToHost, s));
-                HIP_TRY(hipMemcpyAsync(cn, cnt, sizeof(cn), hipMemcpyDeviceToHost, s));
-                HIP_TRY(hipStreamSynchronize(s));
-                const double r = h[10] ? (double)h[10] : 1.0;
-                fprintf(stderr,
-                        "[dense] in=%d out=%d done=%llu iters(ph1)=%llu ph2=%llu | cycles/robot: stage %.0f "
-                        "gam %.0f h0 %.0f solve %.0f test %.0f ph2 %.0f out %.0f | per ph1 iter: solve %.0f test %.0f"
-                        " | all solves: build %.0f (wz %.0f mfma %.0f rows %.0f) chol %.0f subst %.0f\n",
-                        cn[0], cn[8], h[10], h[8], h[9], h[0] / r, h[1] / r, h[2] / r, h[3] / r, h[4] / r,
-                        h[5] / r, h[6] / r, h[3] / (double)(h[8] ? h[8] : 1), h[4] / (double)(h[8] ? h[8] : 1),
-                        (double)(h[11] + h[14] + h[15]) / r, (double)h[14] / r, (double)h[15] / r,
-                        (double)h[11] / r, (double)h[12] / r, (double)h[13] / r);
-                fprintf(stderr, "[dense] ph1 hist:");
-                for (int q = 0; q < 16; q++) fprintf(stderr, " %llu", h[24 + q]);
-                fprintf(stderr, " | ph2 hist:");
-                for (int q = 0; q < 16; q++) fprintf(stderr, " %llu", h[40 + q]);
-                fprintf(stderr, " | cycled %llu\n", h[56]);
-                const double w = h[20] ? (double)h[20] : 1.0;
-                fprintf(stderr, "[fast] waves=%llu per wave: total %.0f back %.0f fwd %.0f iters %.2f | per iter: back %.0f fwd %.0f\n",
-                        h[20], h[19] / w, h[16] / w, h[17] / w, h[18] / w, h[16] / (double)(h[18] ? h[18] : 1),
-                        h[17] / (double)(h[18] ? h[18] : 1));
-            }
-            dbg_sync(s, "dense");
-            left = (const int32_t *)c->retry2.p;
-            left_n = cnt2;
         }
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[2], s));
         // what remains is rare (cycling beyond both, non-finite data): LDS generic kernel, in
-        // the requested arithmetic (the dense tail between is fp64 for both)
+        // the requested arithmetic (the lane-group tail between is fp64 for both)
         // (a refined fp32 request stays fp64 here too: every output it returns is the fp64 optimum)
         if (f32 && !refine)
             HIP_TRY(rmpc_launch_mpc_f32(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
@@ -850,18 +864,19 @@ static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const doubl
     return RMPC_OK;
 }
 
-#if !RMPC_WITH_DENSE
-// The condensed wave-per-robot MFMA tail (csrc/rmpc_mpc_dense.hip, RMPC_TAIL=dense) is an A/B
-// alternative that no default path reaches: it is compiled only by `make DENSE=1`.
-bool rmpc_mpc_dense_supported(int, int, int) { return false; }
-hipError_t rmpc_launch_mpc_dense_f64(const MpcDevParams &, int, int, int, int64_t, const double *, const double *,
-                                     int, const double *, int, const double *, int32_t *, double *, double *,
-                                     double *, double *, int32_t *, uint8_t *, int32_t *, const int32_t *,
-                                     const int32_t *, int32_t *, int32_t *, int32_t *, int, const uint32_t *,
-                                     hipStream_t, unsigned long long *) {
-    return hipErrorInvalidValue;
+static int launch_mpc(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const double *x0,
+                      const double *x_refs, int32_t ref_rows, const double *u_refs, int32_t uref_rows,
+                      const double *obstacles, int32_t n_obs, int32_t *step_count, double *u0,
+                      double *u_seq, double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
+                      int32_t *iters, const int32_t *index, const int32_t *count, hipStream_t s,
+                      const int32_t *ref_off = nullptr, int fast_cap = 0, int warm_shift = 0) {
+    HIP_TRY(order_calls(c, s));
+    const int rc = launch_mpc_impl(c, p, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs, step_count, u0,
+                                   u_seq, x_pred, cost, status, slack_used, iters, index, count, s, ref_off, fast_cap,
+                                   warm_shift);
+    HIP_TRY(mark_call(c, s));
+    return rc;
 }
-#endif
 
 // stage a host array to the device (returns device pointer or nullptr when src is null)
 template <typename T>
@@ -1107,11 +1122,11 @@ extern "C" int rmpc_risk_batch(RmpcCtx *c, const RmpcRiskParams *rp, int64_t B, 
     return RMPC_OK;
 }
 
-static int hybrid_step(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams *lp,
+static int hybrid_step_impl(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams *lp,
                        const RmpcMpcParams *mp, int64_t B, const double *x, const double *x_refs,
                        int32_t ref_rows, const double *u_refs, int32_t uref_rows, const double *obstacles,
                        int32_t n_obs, int32_t *prev_ctrl, int32_t *steps_since, int32_t *step_count,
-                       RmpcLqrCache *cache, double *u_out, uint8_t *used_mpc, double *risk_out, void *stream,
+                            RmpcLqrCache *cache, double *u_out, uint8_t *used_mpc, double *risk_out, void *stream,
                        const int32_t *ref_off, double *pred = nullptr) {
     if (!c || !rp || !lp) return fail(RMPC_EINVAL, "ctx/params is NULL");
     if (!c->sub.empty()) return fail(RMPC_ENOTSUP, "device-pointer entry points take a single-device context");
@@ -1156,10 +1171,15 @@ static int hybrid_step(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams
     }
     LqrDevParams ld = to_dev(lp);
     ld.ref_off = ref_off;
-    HIP_TRY(rmpc_launch_lqr_control(ld, B, x, x_refs, ref_rows * 3, u_refs, uref_rows * 2, cache,
-                                    u_out, nullptr, nullptr, nullptr, nullptr, (const int32_t *)c->idx_lqr.p,
-                                    cnt, side ? c->side : s));
-    if (side) HIP_TRY(hipEventRecord(c->hev[1], c->side));
+    const hipError_t el = rmpc_launch_lqr_control(ld, B, x, x_refs, ref_rows * 3, u_refs, uref_rows * 2, cache,
+                                                  u_out, nullptr, nullptr, nullptr, nullptr,
+                                                  (const int32_t *)c->idx_lqr.p, cnt, side ? c->side : s);
+    const hipError_t eh = side ? hipEventRecord(c->hev[1], c->side) : hipSuccess;
+    if (el != hipSuccess || eh != hipSuccess) {   // no return ahead of the side branch
+        if (side) (void)hipStreamSynchronize(c->side);
+        HIP_TRY(el);
+        HIP_TRY(eh);
+    }
     // MPC branch: solve_with_ltv on the segment; writes u0 straight into u_out
     // the MPC branch holds only the robots near an obstacle: about half the batch, all of
     // them in the hard part of the distribution, so the tail has room for more of them and a
@@ -1169,6 +1189,26 @@ static int hybrid_step(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams
                               (const int32_t *)c->idx_mpc.p, cnt + 1, s, ref_off,
                               c->fast_cap > 0 ? c->fast_cap : (mp->horizon <= 20 && !c->warm_on ? 6 : 0), 1);
     if (side) HIP_TRY(hipStreamWaitEvent(s, c->hev[1], 0));   // join: the step ends when both branches have
+    return rc;
+}
+
+static int hybrid_step(RmpcCtx *c, const RmpcRiskParams *rp, const RmpcLqrParams *lp,
+                       const RmpcMpcParams *mp, int64_t B, const double *x, const double *x_refs,
+                       int32_t ref_rows, const double *u_refs, int32_t uref_rows, const double *obstacles,
+                       int32_t n_obs, int32_t *prev_ctrl, int32_t *steps_since, int32_t *step_count,
+                       RmpcLqrCache *cache, double *u_out, uint8_t *used_mpc, double *risk_out, void *stream,
+                       const int32_t *ref_off, double *pred = nullptr) {
+    if (!c) return fail(RMPC_EINVAL, "ctx/params is NULL");
+    if (!c->sub.empty() || B <= 0)
+        return hybrid_step_impl(c, rp, lp, mp, B, x, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs, prev_ctrl,
+                                steps_since, step_count, cache, u_out, used_mpc, risk_out, stream, ref_off, pred);
+    HIP_TRY(hipSetDevice(c->device));
+    const hipStream_t s = pick(c, stream);
+    HIP_TRY(order_calls(c, s));
+    const int rc = hybrid_step_impl(c, rp, lp, mp, B, x, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
+                                    prev_ctrl, steps_since, step_count, cache, u_out, used_mpc, risk_out, stream,
+                                    ref_off, pred);
+    HIP_TRY(mark_call(c, s));
     return rc;
 }
 

@@ -92,16 +92,6 @@ struct MpcFastArgs {
 bool rmpc_mpc_fast_supported(int N, int bs, int prec, bool lti = false, int no = -1);
 // an fp64 lane-per-robot instance that continues an fp32 request's certified sets
 bool rmpc_mpc_refine_supported(int N, int bs, int no);
-bool rmpc_mpc_dense_supported(int N, int bs, int no);
-hipError_t rmpc_launch_mpc_dense_f64(const MpcDevParams &prm, int N, int bs, int no, int64_t capacity,
-                                     const double *x0, const double *x_refs, int ref_rows,
-                                     const double *u_refs, int uref_rows, const double *obstacles,
-                                     int32_t *step_count, double *u0, double *u_seq, double *x_pred,
-                                     double *cost, int32_t *status, uint8_t *slack_used, int32_t *iters,
-                                     const int32_t *index, const int32_t *count, int32_t *retry,
-                                     int32_t *retry_count, int32_t *next, int pdas_cap,
-                                     const uint32_t *warm, hipStream_t stream,
-                                     unsigned long long *prof = nullptr);
 hipError_t rmpc_launch_mpc_fast(const MpcFastArgs &a, int N, int bs, int prec, hipStream_t stream,
                                 bool lti = false);
 // Diagnostics of the lane-group tail, owned by the context (released with it):

@@ -14,7 +14,7 @@
 // each iteration's per-step hinge weights, set tests, cost terms, hinge forces and box
 // rules run lane-parallel over steps or blocks, and group reductions go through shuffles.
 //
-// Algorithm (identical to the condensed tail in rmpc_mpc_dense.hip, which it replaces):
+// Algorithm (that of the round-1 condensed wave-per-robot tail, which it replaced; HISTORY.md):
 // PDAS from the previous stage's active sets (cap + cycle detection), then projected Newton
 // with an Armijo search along the projection arc, every candidate certified by the
 // set-reproduction test, so the result is the QP's exact optimum.  Robots that do not
@@ -1297,7 +1297,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         const bool pn = phase == PH_PN;
         if (__any(pn)) {
             // projected Newton: gradient at z, epsilon-active box components, hinge rows with
-            // r > 0 -- the sets of this solve (rmpc_mpc_dense.hip phase 2)
+            // r > 0 -- the sets of this solve (projected-Newton phase)
 #if RMPC_GROUP_SCAN
             if constexpr (BS == 1) {
                 gradient(pn, true);

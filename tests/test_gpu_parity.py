@@ -383,20 +383,13 @@ def test_mpc_lti_full_batch_vs_cpu_port(rm):
     np.testing.assert_allclose(out["x_pred"][ok], ref["x_pred"][ok], atol=1e-9, rtol=0)
 
 
-@pytest.mark.parametrize("tail", ["group", "dense"])
-def test_mpc_tail_only_full_batch(rm, monkeypatch, tail):
-    """RMPC_FAST_CAP=0: every one of BASELINE config 3's 65536 robots goes through the tail
-    kernel (16384 lane-group waves / 65536 dense waves, far more than the chip holds at once)
-    -- same results as the C port.  Regression test for the persistent round loop the tails
-    used to have, which faulted from its second round on."""
+def test_mpc_tail_only_full_batch(rm, monkeypatch):
+    """RMPC_FAST_CAP=0: every one of BASELINE config 3's 65536 robots goes through the
+    lane-group tail (16384 waves, far more than the chip holds at once) -- same results as the
+    C port.  Regression test for the persistent round loop the tail used to have, which faulted
+    from its second round on in round 1."""
     monkeypatch.setenv("RMPC_DIAG", "1")   # knobs are read in diagnostics mode only
     monkeypatch.setenv("RMPC_FAST_CAP", "0")
-    if tail == "dense":
-        # the condensed MFMA tail is an A/B alternative built only by `make DENSE=1`
-        with open(rm._native.LIB_PATH, "rb") as f:
-            if b"mpc_dense_kernel" not in f.read():
-                pytest.skip("library built without the dense tail (make DENSE=1)")
-        monkeypatch.setenv("RMPC_TAIL", "dense")
     B, N = 65536, 20
     t0 = (np.arange(B) / B) * (2 * np.pi / 0.5)
     x0, xr, ur = _workload(N, B, 1, t0=t0)
@@ -919,3 +912,96 @@ def test_mpc_warm_start_closed_loop_same_optimum(rm, capsys):
     finally:
         rm.batch.set_warm_start(False, slot=3)
         rm.batch.set_stage_caps(0, 0, slot=3)
+
+
+@pytest.mark.parametrize("N,obs_kind,ltv", [(30, "default", True), (30, "none", True), (10, "default", True),
+                                            (20, "default", False)])
+def test_mpc_fp32_request_unrefined_shapes_are_fp64_exact(rm, N, obs_kind, ltv):
+    """An fp32 request computes in fp32 only where the fp64 refinement re-solves and
+    re-certifies the fp32 active sets (LTV N = 20, and N = 30 with 8 obstacles).  Every other
+    fp32 request -- here N = 30 with the 3 default obstacles or none, N = 10, and LTI -- runs the
+    fp64 pipeline: bitwise the fp64 request's outputs, and the fp64 C port's optimum within
+    1e-9 (so every control an fp32 request returns is the fp64 optimum)."""
+    B = 2048
+    x0, xr, ur = _workload(N, B, 6, t0=(np.arange(B) / B) * (2 * np.pi / 0.5))
+    obs = ompc.default_obstacles() if obs_kind == "default" else np.zeros((0, 3))
+    sc = np.full(B, 10, np.int32)
+    o = {}
+    for prec in (0, 1):
+        p = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02,
+                                  ltv=ltv, precision=prec)
+        o[prec] = rm.batch.mpc_solve_batch(p, x0, xr, ur, obs, step_count=sc.copy())
+    for k in ("u0", "u_seq", "x_pred", "cost", "status", "iters"):
+        np.testing.assert_array_equal(o[1][k], o[0][k])
+    cp = cpu.mpc_params(N, (15, 15, 50), (.1, .1), (30, 30, 40), 0.3, 5000., 2., 3., 0.02, ltv=ltv)
+    ref = cpu.mpc_solve_batch(cp, x0, xr, ur, obs, step_count=sc.copy(), threads=8)
+    both = (o[1]["status"] == 0) & (ref["status"] == 0)
+    assert both.mean() >= 0.99
+    assert np.abs(o[1]["u_seq"][both] - ref["u_seq"][both]).max() <= 1e-9
+    assert np.abs(o[1]["x_pred"][both] - ref["x_pred"][both]).max() <= 1e-9
+
+
+def test_consecutive_calls_on_different_streams_keep_stream_order(rm):
+    """A context's consecutive calls share device state (list counters, the hybrid step's
+    counter pairs, warm-start sets and stamps) and the caller's per-robot state.  Calls issued on
+    alternating streams wait for the previous call (the context's last-call event), so they give
+    bitwise the results of the same calls on one stream: four hybrid steps (config 5's shape)
+    and six warm-started MPC solves (config 3's shape)."""
+    import torch
+    from rmpc import workloads as W
+    B, N = 4096, 20
+    idx = np.arange(B)
+    dev = torch.device("cuda:0")
+    xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, W.cfg5_t0(idx), N + 1)
+    x = xr[:, 0] + W.noise_at(idx, 3)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)          # noqa: E731
+    xs, xrs, urs, obs = d(x), d(xr), d(ur), d(np.asarray(W.DEFAULT_OBS))
+    rp = rm._native.risk_params()
+    lp = rm._native.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0, use_cache=False)
+    mp = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+    s1, s2 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+
+    def hybrid(streams, slot):
+        st = dict(prev_ctrl=torch.full((B,), -1, dtype=torch.int32, device=dev),
+                  steps_since=torch.zeros(B, dtype=torch.int32, device=dev),
+                  step_count=torch.full((B,), 10, dtype=torch.int32, device=dev),
+                  cache=torch.zeros(B * rm._native.LQR_CACHE_DTYPE.itemsize, dtype=torch.uint8, device=dev))
+        torch.cuda.synchronize()
+        res = []
+        for k in range(4):
+            u = torch.empty(B, 2, dtype=torch.float64, device=dev)
+            used = torch.empty(B, dtype=torch.uint8, device=dev)
+            risk = torch.empty(B, dtype=torch.float64, device=dev)
+            rm.batch.hybrid_step_batch_dev(rp, lp, mp, xs, xrs, urs, obs, st, u, used, risk,
+                                           stream=streams[k % len(streams)], slot=slot)
+            res.append((u, used, risk))
+        torch.cuda.synchronize()
+        return [[t.cpu().numpy() for t in r] for r in res]
+
+    def warm_mpc(streams, slot):
+        rm.batch.set_warm_start(True, slot=slot)
+        sc = torch.full((B,), 10, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        res = []
+        for k in range(6):
+            out = dict(u0=torch.empty(B, 2, dtype=torch.float64, device=dev),
+                       u_seq=torch.empty(B, N, 2, dtype=torch.float64, device=dev),
+                       status=torch.empty(B, dtype=torch.int32, device=dev),
+                       iters=torch.empty(B, dtype=torch.int32, device=dev))
+            rm.batch.mpc_solve_batch_dev(mp, xs, xrs, urs, obs, out, step_count=sc,
+                                         stream=streams[k % len(streams)], slot=slot)
+            res.append(out)
+        torch.cuda.synchronize()
+        rm.batch.set_warm_start(False, slot=slot)
+        return [{k: v.cpu().numpy() for k, v in r.items()} for r in res]
+
+    a, b = hybrid([s1], 5), hybrid([s1, s2], 6)
+    for ra, rb in zip(a, b):
+        for ta, tb in zip(ra, rb):
+            np.testing.assert_array_equal(ta, tb)
+    assert 0.2 < a[0][1].mean() < 0.8
+    a, b = warm_mpc([s1], 7), warm_mpc([s1, s2], 8)
+    for ra, rb in zip(a, b):
+        for k in ra:
+            np.testing.assert_array_equal(ra[k], rb[k])
+    assert a[-1]["iters"].mean() < a[0]["iters"].mean()
