@@ -313,6 +313,7 @@ def main():
                     help="MPCController.solve (absolute-state LTI, mpc_node's path) instead of solve_with_ltv")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-closed-loop", action="store_true", help="skip the closed-loop (cold / warm) rates")
+    ap.add_argument("--no-drop-in", action="store_true", help="skip the single-robot drop-in latency")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline work budget")
     ap.add_argument("--stage-caps", default=None,
                     help="FAST,TAIL: the in-flight contexts' stage caps instead of the tuned ones (sweeps)")
@@ -580,6 +581,11 @@ def main():
     if world == 1 and rank == 0 and args.config in ("cfg3", "cfg4") and not args.lti and not args.no_closed_loop:
         line["closed_loop"] = closed_loop(dev, B, obs_list, N, f32)
 
+    # ---- single-robot drop-in latency (rank 0, N=1, config 3 runs only; never `value`)
+    seqs = None
+    if world == 1 and rank == 0 and args.config == "cfg3" and not args.lti and not args.no_drop_in:
+        line["drop_in_latency"], seqs = drop_in_latency(local)
+
     # ---- CPU baseline (rank 0, N=1 only): the oracle's C restatement of the same algorithm
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         from oracle import cpu
@@ -638,6 +644,19 @@ def main():
                                             "and re-solves / re-certifies them in fp64 (outputs fp64-exact)")
         line["max_abs_du_vs_cpu_port"] = du
         line["max_abs_diff_vs_cpu_port_per_fleet"] = du_fleet
+        if seqs:
+            # the C port, one thread, one robot per call, on the drop-in loop's own inputs
+            for (Nd, bs), (xs, xrs, urs) in seqs.items():
+                cpd = cpu.mpc_params(Nd, (15, 15, 50), (.1, .1), (30, 30, 40), 0.3, 5000., 2., 3., 0.02,
+                                     block_size=bs)
+                sc1 = np.full(1, 10, np.int32)
+                ts = []
+                for k in range(len(xs)):
+                    t = time.perf_counter()
+                    cpu.mpc_solve_batch(cpd, xs[k:k + 1], xrs[k:k + 1], urs[k:k + 1], W.DEFAULT_OBS, step_count=sc1,
+                                        threads=1)
+                    ts.append(time.perf_counter() - t)
+                line["drop_in_latency"][f"N{Nd}_bs{bs}"]["cpu_port_1thread_median_us"] = float(np.median(ts[10:])) * 1e6
     # HBM traffic per launch from the committed PMC passes of this workload (rocprofv3 --pmc
     # FETCH_SIZE / WRITE_SIZE in separate runs, gfx950 corrections: scripts/pmc_traffic.py)
     if args.config == "cfg3" and not args.lti and not f32:
@@ -661,6 +680,52 @@ def main():
         dist.destroy_process_group()
 
 
+
+
+REF_LOGGED_SOLVE_MS = 82.6   # mean solve_time_ms of logs/controls_20260208_014109.csv
+
+
+def drop_in_latency(local, n_calls=200, skip=10):
+    """The reference's own performance figure is one robot's per-solve latency (solve_time_ms,
+    mpc_controller.py:360, 482; 82.6 ms mean in logs/controls_20260208_014109.csv, CVXPY/OSQP,
+    N = 6).  Here: rmpc.MPCController.solve_with_ltv for ONE robot through the host-array C-ABI
+    (numpy in, numpy out, synchronous), the reference's controller settings, warm start on (the
+    controller's own context, as the reference solves with warm_start=True), closed loop along
+    the Figure-8 with the plant stepped between solves (untimed), at run_simulation.py's N = 6 /
+    bs = 2 (:164-176) and at config 1's N = 20.  Wall clock per call, after `skip` calls.
+    Returns the latencies and the (x0, x_refs, u_refs) sequence of each size."""
+    import numpy as np
+    import rmpc
+    from rmpc import workloads as W
+    res, seqs = {}, {}
+    for N, bs in ((6, 2), (20, 1)):
+        c = rmpc.MPCController(horizon=N, Q_diag=[15, 15, 50], R_diag=[.1, .1], P_diag=[30, 30, 40],
+                               d_safe=0.3, slack_penalty=5000.0, v_max=2.0, omega_max=3.0, dt=0.02,
+                               block_size=bs, device=local)
+        xr_all, ur_all = rmpc.batch.figure8_batch(np.arange(n_calls) * 0.02, N + 1, device=local)
+        x = xr_all[0, 0] + np.array([0.05, -0.05, 0.1])
+        obs = [rmpc.Obstacle(*o) for o in W.DEFAULT_OBS]
+        ts, rep, its, seq = [], [], [], []
+        for k in range(n_calls):
+            t = time.perf_counter()
+            s = c.solve_with_ltv(x, xr_all[k], ur_all[k], obs)
+            ts.append(time.perf_counter() - t)
+            rep.append(s.solve_time_ms)
+            its.append(s.iterations)
+            seq.append(x.copy())
+            assert s.status == "optimal"
+            x = rmpc.batch.plant_step_batch(x[None], s.optimal_control[None], 0.02, 2.0, 3.0, device=local)[0]
+        us = np.asarray(ts[skip:]) * 1e6
+        res[f"N{N}_bs{bs}"] = {"median_us": float(np.median(us)), "p90_us": float(np.percentile(us, 90)),
+                               "solve_time_ms_median": float(np.median(rep[skip:])),
+                               "iters_mean": float(np.mean(its[skip:])), "calls": n_calls - skip,
+                               "vs_reference_logged_mean": REF_LOGGED_SOLVE_MS * 1e3 / float(np.median(us))}
+        seqs[(N, bs)] = (np.asarray(seq), xr_all, ur_all)
+    res["reference_logged_mean_ms"] = REF_LOGGED_SOLVE_MS
+    res["note"] = ("one robot per call: MPCController.solve_with_ltv (host numpy in/out, 3 kernel launches, "
+                   "synchronous), closed loop on the Figure-8 with 3 obstacles, warm start on; the reference's "
+                   "82.6 ms is CVXPY/OSQP at N=6 on unstated hardware")
+    return res, seqs
 
 
 def closed_loop(dev, B, obs_list, N=20, f32=False, K=50, fleets_max=3, hybrid=False, t0=None):

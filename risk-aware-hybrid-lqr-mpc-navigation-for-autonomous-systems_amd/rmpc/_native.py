@@ -186,6 +186,20 @@ def context(device=0, slot=0):
     return ctx
 
 
+def own_context(device=0):
+    """A context of its own for one caller (an MPCController instance: its warm-start sets
+    belong to that controller).  Release it with release_context."""
+    lib = load()
+    h = _vp()
+    check(lib.rmpc_ctx_create(int(device), C.byref(h)), "rmpc_ctx_create")
+    return h
+
+
+def release_context(h):
+    if h is not None and _lib is not None:
+        _lib.rmpc_ctx_destroy(h)
+
+
 def ptr(a):
     """Data pointer of a C-contiguous numpy array or torch tensor (None -> NULL)."""
     if a is None:

@@ -22,11 +22,12 @@ def _obs(obstacles):
 
 
 def mpc_solve_batch(params, x0, x_refs, u_refs, obstacles=None, step_count=None, device=0,
-                    want_seq=True, slot=0):
+                    want_seq=True, slot=0, ctx=None):
     """MPCController.solve_with_ltv / solve for B robots (mpc_controller.py:150-522).
 
     x0 [B,3]; x_refs [B,R,3]; u_refs [B,U,2]; obstacles [n_obs,3]; step_count [B] int32
     (updated in place, LTV).  Returns dict u0, u_seq, x_pred, cost, status, slack_used, iters.
+    ctx: a context of the caller's own (nat.own_context) instead of the shared (device, slot) one.
     """
     lib = nat.load()
     x0 = f64(x0)
@@ -46,7 +47,8 @@ def mpc_solve_batch(params, x0, x_refs, u_refs, obstacles=None, step_count=None,
         if not (isinstance(step_count, np.ndarray) and step_count.dtype == np.int32
                 and step_count.shape == (B,) and step_count.flags.c_contiguous):
             raise ValueError("step_count must be a C-contiguous int32 array of shape [B]")
-    ctx = nat.context(device, slot)
+    if ctx is None:
+        ctx = nat.context(device, slot)
     check(lib.rmpc_mpc_solve_batch(ctx, C.byref(params), B, ptr(x0), ptr(x_refs), x_refs.shape[1],
                                    ptr(u_refs), u_refs.shape[1], ptr(obs), obs.shape[0],
                                    ptr(step_count), ptr(out["u0"]), ptr(out["u_seq"]),

@@ -70,7 +70,7 @@ class MPCController:
     def __init__(self, horizon: int = 10, Q_diag: list = None, R_diag: list = None,
                  P_diag: list = None, d_safe: float = 0.3, slack_penalty: float = 5000.0,
                  v_max: float = 1.0, omega_max: float = 1.5, dt: float = 0.02,
-                 solver: str = "OSQP", block_size: int = 1, device: int = 0):
+                 solver: str = "OSQP", block_size: int = 1, device: int = 0, warm_start: bool = True):
         self.N = horizon
         self.dt = dt
         self.d_safe = d_safe
@@ -91,6 +91,12 @@ class MPCController:
         self.P = np.diag(P_diag)
         self.linearizer = Linearizer(dt=dt)            # mpc_controller.py:136 (API surface)
         self.device = device
+        # The reference solves with warm_start=True (mpc_controller.py:276-277, 474-475): here
+        # each controller owns a library context whose warm-start sets are this robot's
+        # previous certified active sets (rmpc_ctx_set_warm_start), shifted by one step.  Same
+        # optimum, fewer PDAS iterations.  warm_start=False: the shared context, cold solves.
+        self.warm_start = warm_start
+        self._ctx = None
         self._prev_solution: Optional[np.ndarray] = None
         self._prev_states: Optional[np.ndarray] = None
         self._step_count = 0
@@ -105,6 +111,21 @@ class MPCController:
                               block_size=self.block_size if ltv else 1, ltv=ltv, soft=soft,
                               ramp_up_steps=self._ramp_up_steps)
 
+    def _context(self):
+        if not self.warm_start:
+            return None
+        if self._ctx is None:
+            self._ctx = nat.own_context(self.device)
+            nat.check(nat.load().rmpc_ctx_set_warm_start(self._ctx, 1), "rmpc_ctx_set_warm_start")
+        return self._ctx
+
+    def __del__(self):
+        ctx, self._ctx = getattr(self, "_ctx", None), None
+        try:
+            nat.release_context(ctx)
+        except Exception:   # noqa: BLE001  (interpreter shutdown)
+            pass
+
     # -------------------------------------------------------------- single robot
     def _one(self, x0, x_refs, u_refs, obstacles, soft, ltv):
         t = time.perf_counter()
@@ -113,7 +134,7 @@ class MPCController:
         sc = np.array([self._step_count], np.int32)
         out = mpc_solve_batch(self._params(ltv, soft), np.asarray(x0, np.float64)[None],
                               x_refs[None], u_refs[None], _obstacle_array(obstacles),
-                              step_count=sc if ltv else None, device=self.device)
+                              step_count=sc if ltv else None, device=self.device, ctx=self._context())
         ms = (time.perf_counter() - t) * 1000.0
         st = int(out["status"][0])
         if st != nat.RMPC_FALLBACK:
@@ -189,6 +210,8 @@ class MPCController:
         self._step_count = 0
         self._prev_solution = None
         self._prev_states = None
+        if self._ctx is not None:           # cold sets again (reset: mpc_controller.py:548-552)
+            nat.check(nat.load().rmpc_ctx_set_warm_start(self._ctx, 1), "rmpc_ctx_set_warm_start")
 
     def _clip_control(self, u: np.ndarray) -> np.ndarray:
         return np.array([np.clip(u[0], -self.v_max, self.v_max),

@@ -119,14 +119,20 @@ def test_mpc_ltv_drop_in_vs_logged_osqp(rm, golden):
     kw = dict(horizon=6, Q_diag=[15, 15, 50], R_diag=[.1, .1], P_diag=[30, 30, 40], d_safe=0.3,
               slack_penalty=5000.0, v_max=2.0, omega_max=3.0, dt=0.02, solver="OSQP",
               block_size=2)
-    c = rm.MPCController(**kw)
+    c = rm.MPCController(**kw)                        # warm_start=True, as the reference solves
+    cc = rm.MPCController(**kw, warm_start=False)      # cold: every solve from empty sets
     oc = ompc.MPCController(**kw)
-    err_log, err_orc, slack = [], [], []
+    err_log, err_orc, slack, it_w, it_c = [], [], [], 0, 0
     for k, x0, u0 in zip(d["k"], d["x0"], d["u0"]):
         xr, ur = g.segment(int(k), 7)
         s = c.solve_with_ltv(x0, xr, ur, [rm.Obstacle(*o) for o in ompc.default_obstacles()])
+        sc = cc.solve_with_ltv(x0, xr, ur, [rm.Obstacle(*o) for o in ompc.default_obstacles()])
         so = oc.solve_with_ltv(x0, xr, ur, ompc.default_obstacles())
-        assert s.status == "optimal"
+        assert s.status == "optimal" and sc.status == "optimal"
+        # the warm start changes the iterations, not the certified optimum
+        assert np.abs(s.control_sequence - sc.control_sequence).max() <= 1e-12
+        assert np.abs(s.predicted_states - sc.predicted_states).max() <= 1e-12
+        it_w, it_c = it_w + s.iterations, it_c + sc.iterations
         err_log.append(np.abs(s.optimal_control - u0).max())
         err_orc.append(max(np.abs(s.control_sequence - so.control_sequence).max(),
                            np.abs(s.predicted_states - so.predicted_states).max()))
@@ -134,7 +140,8 @@ def test_mpc_ltv_drop_in_vs_logged_osqp(rm, golden):
         assert s.slack_used == so.slack_used
         assert abs(s.cost - so.cost) <= 1e-9 * max(1.0, abs(so.cost))
     err_log, err_orc, slack = map(np.array, (err_log, err_orc, slack))
-    assert c._step_count == 200
+    assert c._step_count == 200 and cc._step_count == 200
+    assert it_w < it_c, (it_w, it_c)                  # per-controller warm start (own context)
     assert np.all(err_orc <= 1e-9)
     assert (err_log <= 1e-9).sum() >= 189 and np.all(err_log[~slack] <= 1e-9)
     assert np.all(err_log <= 2e-3)        # OSQP's own error on slack-active solves
