@@ -657,29 +657,38 @@ def main():
                                         threads=1)
                     ts.append(time.perf_counter() - t)
                 line["drop_in_latency"][f"N{Nd}_bs{bs}"]["cpu_port_1thread_median_us"] = float(np.median(ts[10:])) * 1e6
-    # HBM traffic per launch from the committed PMC passes of this workload (rocprofv3 --pmc
-    # FETCH_SIZE / WRITE_SIZE in separate runs, gfx950 corrections: scripts/pmc_traffic.py)
-    if args.config == "cfg3" and not args.lti and not f32:
-        tr, src = latest_profile("pmc_traffic.json")
-        if tr:
-            line["roofline"]["traffic"] = tr["traffic_bytes_per_launch"]
-            line["roofline"]["traffic_unit"] = f"bytes/launch (PMC, {src})"
-            line["roofline"]["traffic_vs_algorithmic"] = tr["traffic_bytes_per_launch"] / (abytes * B)
-        # executed flops per launch from the PMC fp64 VALU counters of this workload
-        fl, src = latest_profile("pmc_flops.json")
-        if fl:
-            ex = fl["fp64_flops_per_launch"]
-            line["roofline"]["executed_flops_per_launch"] = ex
-            line["roofline"]["achieved_executed"] = ex / k_avg_s / 1e12
-            line["roofline"]["frac_executed"] = ex / k_avg_s / 1e12 / peak
-            line["roofline"]["executed_source"] = (f"{src}: 64 x (2 FMA + ADD + MUL + TRANS) fp64 VALU "
-                                                   "instructions (full-wave count: an upper bound)")
+    # HBM traffic and executed flops per launch from the committed PMC passes of this workload
+    # (rocprofv3 --pmc, separate passes; scripts/pmc_hbm.sh, scripts/pmc_flops.sh)
+    if not args.lti and not args.f32 and not args.f64 and args.config in ("cfg3", "cfg4"):
+        pmc_into_roofline(line["roofline"], "" if args.config == "cfg3" else "_" + args.config, abytes * B, k_avg_s)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
 
 
+
+
+def pmc_into_roofline(roof, suffix, alg_bytes, k_avg_s):
+    """Fill roofline.traffic (HBM bytes per launch, PMC FETCH_SIZE + WRITE_SIZE with the gfx950
+    corrections) and the executed-flops fraction from the newest committed profiles/r*/
+    pmc_traffic<suffix>.json and pmc_flops<suffix>.json (this workload's own passes).
+    frac_executed prices each precision at its own vector peak: (fp64 / FP64 peak + fp32 / FP32
+    peak) / launch time."""
+    tr, src = latest_profile(f"pmc_traffic{suffix}.json")
+    if tr:
+        roof["traffic"] = tr["traffic_bytes_per_launch"]
+        roof["traffic_unit"] = f"bytes/launch (PMC, {src})"
+        if alg_bytes:
+            roof["traffic_vs_algorithmic"] = tr["traffic_bytes_per_launch"] / alg_bytes
+    fl, src = latest_profile(f"pmc_flops{suffix}.json")
+    if fl:
+        e64, e32 = fl["fp64_flops_per_launch"], fl.get("fp32_flops_per_launch", 0.0)
+        roof["executed_flops_per_launch"] = {"fp64": e64, "fp32": e32}
+        roof["achieved_executed"] = (e64 + e32) / k_avg_s / 1e12
+        roof["frac_executed"] = (e64 / FP64_PEAK_TFLOPS + e32 / FP32_PEAK_TFLOPS) / 1e12 / k_avg_s
+        roof["executed_source"] = (f"{src}: 64 x (2 FMA + ADD + MUL + TRANS) VALU instructions per precision "
+                                   "(full-wave count: an upper bound)")
 
 
 REF_LOGGED_SOLVE_MS = 82.6   # mean solve_time_ms of logs/controls_20260208_014109.csv (BASELINE.md)
@@ -1029,6 +1038,8 @@ def bench_other(args, world, rank, local, dist, pre=None):
                             "mpc_iters_mean": its_mpc,
                             "hbm_gbs_algorithmic": (24 + fm * algorithmic_bytes(N, 3, False) + (1 - fm) * 80) * B
                             / k_avg_s / 1e9}
+        pmc_into_roofline(line["roofline"], "_cfg5", (24 + fm * algorithmic_bytes(N, 3, False) + (1 - fm) * 80) * B,
+                          k_avg_s)
     # ---- CPU baseline (rank 0, N=1): the oracle's C restatement of the same step
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         from oracle import cpu

@@ -7,7 +7,7 @@
 # Usage: bash scripts/measure_round.sh <tag> <profiles dir>   (outputs under gpurun_out/<tag>_*;
 # the PMC jsons are copied into the profiles dir, where bench.py finds the newest)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
-tag=${1:-m}; rdir=${2:-profiles/r03}
+tag=${1:-m}; rdir=${2:-profiles/r04}
 mkdir -p gpurun_out $rdir
 step() { echo "== $(date +%T) $*"; }
 prof() {   # prof <name> <bench args...>: rocprofv3 kernel trace + stats of a short bench run
@@ -16,12 +16,20 @@ prof() {   # prof <name> <bench args...>: rocprofv3 kernel trace + stats of a sh
     -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pcie --no-closed-loop "$@" \
     > gpurun_out/${tag}_prof_${name}_bench.json 2> gpurun_out/${tag}_prof_$name.err || { tail gpurun_out/${tag}_prof_$name.err; exit 1; }
 }
-step pmc hbm
-bash scripts/pmc_hbm.sh ${tag}_hbm > gpurun_out/${tag}_pmc_hbm.log 2>&1 || { tail gpurun_out/${tag}_pmc_hbm.log; exit 1; }
-cp gpurun_out/${tag}_hbm_traffic.json $rdir/pmc_traffic.json
-step pmc flops
-bash scripts/pmc_flops.sh ${tag}_fl > gpurun_out/${tag}_pmc_flops.log 2>&1 || { tail gpurun_out/${tag}_pmc_flops.log; exit 1; }
-cp gpurun_out/${tag}_fl_flops.json $rdir/pmc_flops.json
+# PMC passes per configuration (entry kernel = the first kernel of each library call); the
+# jsons land in the profiles dir as pmc_{traffic,flops}[_cfgN].json, where bench.py finds them
+pmc() {   # pmc <suffix> <entry kernel> <bench args...>
+  local sfx=$1 entry=$2; shift; shift
+  step pmc hbm $sfx
+  bash scripts/pmc_hbm.sh ${tag}_hbm$sfx "$entry" "$@" > gpurun_out/${tag}_pmc_hbm$sfx.log 2>&1 || { tail gpurun_out/${tag}_pmc_hbm$sfx.log; exit 1; }
+  cp gpurun_out/${tag}_hbm${sfx}_traffic.json $rdir/pmc_traffic$sfx.json
+  step pmc flops $sfx
+  bash scripts/pmc_flops.sh ${tag}_fl$sfx "$entry" "$@" > gpurun_out/${tag}_pmc_flops$sfx.log 2>&1 || { tail gpurun_out/${tag}_pmc_flops$sfx.log; exit 1; }
+  cp gpurun_out/${tag}_fl${sfx}_flops.json $rdir/pmc_flops$sfx.json
+}
+pmc "" mpc_ltv_fast_kernel
+pmc _cfg4 "mpc_ltv_fast_kernel<30, 1, float" --config cfg4 --inflight 1
+pmc _cfg5 hybrid_decide_kernel --config cfg5 --inflight 1
 step bench cfg3
 timeout -k 10 600 python bench.py > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || { tail gpurun_out/${tag}_bench.err; exit 1; }
 for c in cfg2 cfg4 cfg5; do
