@@ -149,7 +149,7 @@ int rmpc_ctx_set_timing(RmpcCtx *ctx, int32_t on);
  * stage before a robot moves to the lane-group tail, and PDAS solves in the tail before
  * projected Newton.  0 = the library default (7 / 4 at N <= 20).  With several batches in
  * flight on several contexts, a longer first stage moves less work into the tail
- * ((9, 4) at BASELINE configs 3 and 5).  They apply to the hybrid
+ * (HISTORY.md section 1: (9, 4) at BASELINE configs 3 and 5).  They apply to the hybrid
  * step's MPC branch too (its default first-stage cap is 6).  fast_cap, tail_cap in [0, 64]. */
 int rmpc_ctx_set_stage_caps(RmpcCtx *ctx, int32_t fast_cap, int32_t tail_cap);
 /* Side stream on this context (a performance setting; results are identical): on (default),
@@ -158,7 +158,7 @@ int rmpc_ctx_set_stage_caps(RmpcCtx *ctx, int32_t fast_cap, int32_t tail_cap);
  * forked from and joined back to the call's stream.  Off, the branches run in order on the
  * call's stream.  With several contexts in flight on their own streams, the side streams add
  * to the streams sharing the device's hardware queues (GPU_MAX_HW_QUEUES), and the other
- * batches already fill the chip: the bench turns them off there. */
+ * batches already fill the chip: the bench turns them off there (HISTORY.md section 1). */
 int rmpc_ctx_set_side_stream(RmpcCtx *ctx, int32_t on);
 /* Warm start across calls on this context (replaces the reference's warm_start=True solves
  * with get_warm_start's shifted previous solution, mpc_controller.py:272-277, 470-475,

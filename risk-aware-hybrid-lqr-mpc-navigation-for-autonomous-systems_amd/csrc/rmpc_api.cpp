@@ -145,7 +145,7 @@ struct RowArr {
 // Robots of shard d of n: blocks of RMPC_SPLIT_BLOCK consecutive robots dealt round-robin
 // (block k to shard k mod n).  Robot difficulty follows the Figure-8 phase, which varies
 // slowly with the robot index, so every shard gets the batch's mix (a contiguous split
-// hands the obstacle-adjacent arcs to a few devices: DESIGN.md section 7).
+// hands the obstacle-adjacent arcs to a few devices: HISTORY.md section 7).
 #define RMPC_SPLIT_BLOCK 64
 
 // Runs fn(sub_ctx, B_d, shard_pointers) for every device concurrently (one host thread
@@ -224,7 +224,7 @@ int rmpc_ctx_create(int device_id, RmpcCtx **out) {
     // used only through the _dev entry points: creating it on first use measured slower with
     // batches in flight (config 4 68.0M against 70.1M, config 5 402M against 419M solves/s) --
     // the streams of a process share GPU_MAX_HW_QUEUES hardware queues, and which ones share
-    // depends on the order they are made
+    // depends on the order they are made (HISTORY.md section 1)
     if (!own(c)) {
         delete c;
         return fail(RMPC_EHIP, "hipStreamCreate failed");
@@ -629,12 +629,7 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
                                               : (p->horizon <= 20 ? (lti ? 9 : 7) : 12);
         const bool warm = !rmpc_knob("RMPC_COLD_TAIL");
         a.init_zc = rmpc_knob("RMPC_INIT_ZC") ? atoi(rmpc_knob("RMPC_INIT_ZC")) : 0;
-        // RMPC_STRAGGLE=it,lanes (A/B): straggler hand-off (MpcFastArgs::straggle_it)
-        if (const char *sg = rmpc_knob("RMPC_STRAGGLE")) {
-            a.straggle_it = atoi(sg);
-            const char *q = strchr(sg, ',');
-            a.straggle_lanes = q ? atoi(q + 1) : 4;
-        }
+
         if (warm) {
             HIP_TRY(c->retry_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
             a.retry_sets = (uint32_t *)c->retry_sets.p;
@@ -690,7 +685,7 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
         // that a later pass's wave holds no robot that has already finished: at BASELINE
         // config 3, 67% of the robots certify in their first solve, but a 64-robot wave almost
         // always holds one that needs 3-7.  (RMPC_FAST_SPLIT=c1[,c2[,c3]]: the earlier passes'
-        // caps, A/B only; default one pass)
+        // caps, A/B only; default one pass, HISTORY.md section 4)
         int splits[3], nsplit = 0;
         if (const char *sp = rmpc_knob("RMPC_FAST_SPLIT")) {
             for (const char *q = sp; *q && nsplit < 3;) {

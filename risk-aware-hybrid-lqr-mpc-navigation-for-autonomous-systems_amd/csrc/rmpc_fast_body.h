@@ -529,11 +529,6 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
         else gt.ld(j, dst);
     };
     while (fin && it < maxit) {
-        // straggler hand-off (MpcFastArgs::straggle_it): the few robots of this wave still
-        // iterating go to the lane-group tail now instead of holding the SIMD to the cap
-        // (one lane per robot only: the paired fp64 instance has no register to spare)
-        if constexpr (PR == 1)
-            if (a.straggle_it > 0 && it >= a.straggle_it && __popcll(__ballot(1)) <= a.straggle_lanes) break;
         it++;
         // Keep the per-step inputs opaque to the optimiser at every iteration: otherwise it
         // hoists everything derived from them (hinge normals of every row, linearisation

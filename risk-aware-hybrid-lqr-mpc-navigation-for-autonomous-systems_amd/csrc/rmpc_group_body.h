@@ -1445,7 +1445,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
             // Every global load of the pass is issued before its first store: gfx950 counts
             // loads and stores in one in-order vmcnt, so a load behind the u_seq / x_pred
             // stores would wait for all of them to complete (the lane-per-robot kernel's
-            // output pass)
+            // output pass, HISTORY.md section 3)
             constexpr int KU = (N + G - 1) / G, KX = (N + 1 + G - 1) / G;
             double urv[F64 ? 1 : KU][2], xrv[LTI ? 1 : KX][3];
             if constexpr (!F64) {

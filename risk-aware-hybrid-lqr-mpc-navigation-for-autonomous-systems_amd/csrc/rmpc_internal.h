@@ -85,9 +85,6 @@ struct MpcFastArgs {
     uint32_t *prev_sets;
     int prev_shift;
     uint32_t prev_stamp;
-    // Straggler hand-off: from PDAS iteration straggle_it on, a wave whose robots still iterating
-    // number at most straggle_lanes hands them on at once (0: off)
-    int straggle_it, straggle_lanes;
     // Overlapped pipeline (rmpc_mpc_pipe.hip): each retry entry is published by storing
     // ready_stamp into ready[slot] (agent-scope release) once its robot and sets are written;
     // null: the stage kernels, no publishing

@@ -76,7 +76,7 @@ void GroupDiag::release() {
 
 // fp32 instances (the LTV fp32 fast instances' shapes, N = 20 / 30): opt-in, RMPC_TAIL32=1.
 // Faster than the fp64 tail at config 4 (42.9M against 38.7M solves/s) since packed-fp32 code
-// is no longer generated, but with every robot routed through it the
+// is no longer generated (HISTORY.md section 4), but with every robot routed through it the
 // fp32 tail's control error reached 1.9e-4 relative, above the north star's 1e-4.
 bool rmpc_mpc_group_supported(int N, int bs, int no, bool f32) {
     if (f32 && !(bs == 1 && (N == 20 || N == 30) && rmpc_knob("RMPC_TAIL32") && atoi(rmpc_knob("RMPC_TAIL32")) > 0))

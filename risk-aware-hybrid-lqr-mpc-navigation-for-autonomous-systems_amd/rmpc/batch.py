@@ -228,7 +228,7 @@ def set_stage_timing(on=True, device=0):
 def set_stage_caps(fast_cap=0, tail_cap=0, device=0, slot=0):
     """MPC pipeline stage caps of one context (rmpc_ctx_set_stage_caps; 0 = library default):
     PDAS solves in the lane-per-robot stage, then in the lane-group tail.  Same optimum either
-    way; a longer first stage suits several batches in flight."""
+    way; a longer first stage suits several batches in flight (HISTORY.md section 1)."""
     lib = nat.load()
     check(lib.rmpc_ctx_set_stage_caps(nat.context(device, slot), int(fast_cap), int(tail_cap)),
           "rmpc_ctx_set_stage_caps")

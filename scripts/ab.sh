@@ -13,7 +13,7 @@ steps=${STEPS:-30}
 for v in "$@"; do
   [ "$v" = "-" ] && v=""
   tag=$(echo "$args $v" | tr -c 'a-zA-Z0-9' '_' | cut -c1-120)
-  env $v timeout -k 10 240 python bench.py $args --steps $steps --warmup 3 --no-cpu-baseline --no-pcie --no-closed-loop \
+  env $v timeout -k 10 240 python bench.py $args --steps $steps --warmup 3 --no-cpu-baseline --no-pcie --no-closed-loop --no-drop-in \
       > gpurun_out/ab_$tag.json 2>gpurun_out/ab_$tag.err || { echo "[$args | $v] failed"; tail -5 gpurun_out/ab_$tag.err; exit 1; }
   python -c "
 import json;d=json.load(open('gpurun_out/ab_$tag.json'));r=d.get('roofline',{})

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Root-cause probe for the round-2 packed-fp32 wrong-result defect.
+# Root-cause probe for the round-2 packed-fp32 wrong-result defect (HISTORY.md section 4).
 #
 # Builds, HERE (no GPU needed), variants of librmpc from a given commit's sources into
 # probe/ (git-ignored .so files, which travel to the GPU box):

@@ -115,7 +115,7 @@ def test_library_has_no_packed_fp32_code(lib, tmp_path):
     In round 2 an fp32 build with packed code certified wrong controls for 29-32 of 2048 robots
     (lanes 12-15 of lane rows 1-3) depending on the instruction schedule; the library is built
     with -fno-slp-vectorize -fno-vectorize, the two passes that emitted packed fp32 (the
-    Makefile).  This guards against a toolchain update or a code change
+    Makefile; HISTORY.md section 4).  This guards against a toolchain update or a code change
     bringing such code back unnoticed."""
     if not os.path.exists(f"{LLVM_BIN}/llvm-objdump"):
         pytest.skip("no llvm-objdump")
