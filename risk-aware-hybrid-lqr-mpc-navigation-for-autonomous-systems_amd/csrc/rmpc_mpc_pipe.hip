@@ -11,19 +11,24 @@
 // launch between the stages is gone.
 //
 // Hand-off protocol (agent scope; MI355X has one L2 per XCD):
-//   producer (fast_body's hand-on): reserve a slot (atomicAdd on the list count), store the
-//     robot and its sets, release fence + vmcnt(0), store the call's stamp into ready[slot];
-//     after its stage every wave releases and adds 1 to `done`.
-//   consumer: claims a run of reserved slots with a CAS on `head` (never past the count), waits
-//     for each claimed slot's stamp (its producer is running and never waits, so the wait is
-//     short), acquires, then reads the entry.
-// Forward progress: a wave waits for work only when every wave of the grid has started
-// (`started` == grid), so a waiting wave never keeps a wave of its own grid from being placed;
-// before that it takes only what is already there and leaves.  Producers never wait.  A wave
-// leaves when every wave's stage is done (`done` == grid; the count is then final) and the
-// list is drained.  Every spin is bounded (~0.2 s) as a last-resort guard against a hang.
+//   producer (fast_body<..., PUB>'s hand-on): reserve a slot (atomicAdd on the list count),
+//     store the robot and its sets write-through (agent-scope stores), wait for them (vmcnt(0)),
+//     store the call's stamp into ready[slot]; after its stage every wave waits for its
+//     stores and adds 1 to `done`.  No release fence: at agent scope it writes back the whole
+//     L2, full of the stage's gain tiles (measured: 9 ms instead of 0.34 ms per launch).
+//   consumer: takes a ticket of four slots (one atomic add on `head`), waits for each slot's
+//     stamp, then reads the entry and its sets with agent-scope loads (group_solve<..., SC1>):
+//     no acquire fence, which would invalidate the CU's cached inputs.
+// Forward progress: a wave waits for future hand-ons only when every wave of the grid has
+// started (`started` == grid), so a waiting wave never keeps a wave of its own grid from being
+// placed; before that it claims only reserved slots (CAS, never past the count) and leaves when
+// there are none.  Producers never wait.  A ticket past the final count (`done` == grid) ends
+// the wave.  Every wait is bounded (~0.2 s) as a last-resort guard against a hang.
 #include "rmpc_fast_body.h"
 #include "rmpc_group_body.h"
+
+#include <algorithm>
+#include <vector>
 
 namespace rmpc {
 
@@ -32,6 +37,10 @@ struct PipeCtl {
     int32_t *count;                   // the retry list's count (MpcFastArgs::retry_count)
     const uint32_t *ready;            // per retry slot: the stamp of the call that published it
     uint32_t stamp;
+    int sleep;                        // s_sleep(16) rounds between two polls of a slot's stamp
+    int nowait;                       // 1: never wait for future hand-ons (claim reserved slots only)
+    unsigned long long *diag;         // RMPC_PIPE_DIAG: per wave [start, stage end, rounds, first
+                                      // round start, last round end, exit] (s_memrealtime ticks)
 };
 
 #define RMPC_PIPE_SPIN_TICKS 20000000ull   // s_memrealtime ticks (100 MHz): 0.2 s
@@ -40,33 +49,41 @@ __device__ __forceinline__ int rlx_load(const int32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Lane 0 of a wave: claim up to `want` published-or-reserved retry slots.  Returns the first
-// slot in *h and the number claimed (> 0), or -1: nothing left for this wave.
-__device__ __forceinline__ int pipe_claim(const PipeCtl pc, int want, int *h) {
+// Lane 0 of a wave: the next run of `want` retry slots for this wave, or -1 (leave).
+//  - While not every wave of the grid has started, waiting is not allowed: claim only slots
+//    already reserved (CAS on head, never past the count), else leave.
+//  - Once every wave has started: take a ticket (one atomic add on head).  The slots may not be
+//    reserved yet; the groups wait for them slot by slot (below).  No polling of shared words
+//    here: with ~1000 waves polling one cache line, every claim and every hand-on atomic on that
+//    line queued behind the polls (measured: the tail ran at one round per ~11 us, 9.8 ms per
+//    launch instead of 0.34 ms).
+__device__ __forceinline__ int pipe_claim(const PipeCtl pc, int want) {
     const unsigned waves = gridDim.x;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    if (!pc.nowait && (unsigned)rlx_load(pc.started) >= waves)
+        return __hip_atomic_fetch_add(pc.head, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (;;) {
         const int c = rlx_load(pc.count);
         int hh = rlx_load(pc.head);
-        if (hh < c) {
-            const int n = c - hh < want ? c - hh : want;
-            if (__hip_atomic_compare_exchange_strong(pc.head, &hh, hh + n, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT)) {
-                *h = hh;
-                return n;
-            }
-            continue;
+        if (hh >= c) return -1;
+        if (__hip_atomic_compare_exchange_strong(pc.head, &hh, hh + want < c ? hh + want : c, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return hh;
+    }
+}
+
+// Wait for slot t's stamp.  False when the slot will never be filled: every wave's stage is done
+// (`done` == grid: their hand-ons had completed before they counted, so the count is final) and
+// t is past the count.  The slot's own stamp word is polled (one line per wave's four slots,
+// spread over the chip); the shared `done` word only every 16th poll.  Bounded: 0.2 s.
+__device__ __forceinline__ bool pipe_wait_slot(const PipeCtl pc, int t) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (unsigned i = 0;; i++) {
+        if (__hip_atomic_load(pc.ready + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pc.stamp) return true;
+        if ((i & 15u) == 15u && (unsigned)rlx_load(pc.done) >= gridDim.x) {
+            if (t >= rlx_load(pc.count)) return false;
         }
-        // nothing reserved beyond the head
-        if ((unsigned)__hip_atomic_load(pc.done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= waves) {
-            // every stage has handed on what it will: the count is final
-            if (rlx_load(pc.head) >= rlx_load(pc.count)) return -1;
-            continue;
-        }
-        // waiting is safe only once every wave of the grid has been placed
-        if ((unsigned)rlx_load(pc.started) < waves) return -1;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > RMPC_PIPE_SPIN_TICKS) return -1;
-        __builtin_amdgcn_s_sleep(8);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > RMPC_PIPE_SPIN_TICKS) return false;
+        for (int q = 0; q < pc.sleep; q++) __builtin_amdgcn_s_sleep(16);
     }
 }
 
@@ -74,36 +91,41 @@ template <int N, int BS, typename T, int NO, bool WS, int G>
 __global__ __launch_bounds__(64, 1) void mpc_pipe_kernel(MpcFastArgs fa, GroupArgs ga, PipeCtl pc) {
     constexpr int NB = (N + BS - 1) / BS, RPW = 64 / G;
     const int lane = threadIdx.x;
+    unsigned long long *const dg = pc.diag ? pc.diag + (size_t)blockIdx.x * 8 : nullptr;
+    if (dg && lane == 0) dg[0] = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) __hip_atomic_fetch_add(pc.started, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // ---- stage 1: this wave's robots (hand-ons published slot by slot)
-    fast_body<N, BS, T, false, NO, 1, WS>(fa, blockIdx.x);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    fast_body<N, BS, T, false, NO, 1, WS, true>(fa, blockIdx.x);
+    // every hand-on of this wave has completed (its stamp stores included) before `done` counts it
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) __hip_atomic_fetch_add(pc.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (dg && lane == 0) dg[1] = __builtin_amdgcn_s_memrealtime();
+    unsigned long long rounds = 0;
     // ---- stage 2: lane-group solves of published retry entries, RPW per round
     extern __shared__ double lds_raw[];
     T *const lds = reinterpret_cast<T *>(lds_raw);
     const int gl = lane % G, grp = lane / G;
     const int rec = GRec<N, NB, T>::size(ga.no);
     for (;;) {
-        int h = 0, n = -1;
-        if (lane == 0) n = pipe_claim(pc, RPW, &h);
-        n = __shfl(n, 0);
+        int h = -1;
+        if (lane == 0) h = pipe_claim(pc, RPW);
         h = __shfl(h, 0);
-        if (n < 0) break;
+        if (h < 0) break;
         const int t = h + grp;
-        bool have = grp < n;
-        if (have) {
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            while (__hip_atomic_load(pc.ready + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != pc.stamp) {
-                if (__builtin_amdgcn_s_memrealtime() - t0 > RMPC_PIPE_SPIN_TICKS) { have = false; break; }
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const bool have = pipe_wait_slot(pc, t);
+        if (!__ballot(have)) break;             // a run past the final count: nothing left
+        if (dg && lane == 0 && rounds++ == 0) dg[3] = __builtin_amdgcn_s_memrealtime();
+        // (the entry and its sets are read with agent-scope loads inside group_solve: no acquire
+        // fence, which would drop this CU's cached inputs; only the compiler's order is pinned)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __syncthreads();
-        group_solve<N, BS, G, T, false>(ga, lds + grp * rec, t, have, gl, grp);
+        group_solve<N, BS, G, T, false, true>(ga, lds + grp * rec, t, have, gl, grp);
         __syncthreads();
+        if (dg && lane == 0) dg[4] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (dg && lane == 0) {
+        dg[2] = rounds;
+        dg[5] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -144,6 +166,15 @@ hipError_t rmpc_launch_mpc_pipe(const MpcFastArgs &a, int N, int bs, int32_t *re
     pc.count = a.retry_count;
     pc.ready = a.ready;
     pc.stamp = a.ready_stamp;
+    pc.sleep = rmpc_knob("RMPC_PIPE_SLEEP") ? atoi(rmpc_knob("RMPC_PIPE_SLEEP")) : 1;
+    pc.nowait = rmpc_knob("RMPC_PIPE_NOWAIT") ? 1 : 0;
+    pc.diag = nullptr;
+    const int64_t waves = (n + RMPC_WAVE - 1) / RMPC_WAVE;
+    if (rmpc_knob("RMPC_PIPE_DIAG")) {                  // diagnostics: synchronises the stream
+        const hipError_t e = hipMalloc((void **)&pc.diag, (size_t)waves * 8 * sizeof(unsigned long long));
+        if (e != hipSuccess) return e;
+        (void)hipMemsetAsync(pc.diag, 0, (size_t)waves * 8 * sizeof(unsigned long long), stream);
+    }
     constexpr int G = 16;
     const size_t lds_fast = (size_t)3 * N * RMPC_WAVE * sizeof(double) + (size_t)RMPC_WAVE * 17 * sizeof(double);
     const size_t lds_group = (size_t)(64 / G) * GRec<20, 20, double>::size(a.no) * sizeof(double);
@@ -159,5 +190,31 @@ hipError_t rmpc_launch_mpc_pipe(const MpcFastArgs &a, int N, int bs, int32_t *re
     void *args[] = {&fa, &ga, &pc};
     const hipError_t e = hipLaunchKernel(fn, grid, block, args, lds, stream);
     if (e != hipSuccess) return e;
+    if (pc.diag) {          // per-wave timeline summary, microseconds from the first wave's start
+        std::vector<unsigned long long> h((size_t)waves * 8);
+        hipError_t e2 = hipMemcpyAsync(h.data(), pc.diag, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream);
+        if (e2 == hipSuccess) e2 = hipStreamSynchronize(stream);
+        (void)hipFree(pc.diag);
+        if (e2 != hipSuccess) return e2;
+        unsigned long long t0 = ~0ull;
+        for (int64_t w = 0; w < waves; w++) t0 = std::min(t0, h[w * 8]);
+        auto us = [&](unsigned long long v) { return v ? (double)(v - t0) / 100.0 : -1.0; };
+        std::vector<double> st, se, fr, lr, ex;
+        long long rounds = 0, workers = 0;
+        for (int64_t w = 0; w < waves; w++) {
+            const unsigned long long *r = &h[w * 8];
+            st.push_back(us(r[0])); se.push_back(us(r[1])); ex.push_back(us(r[5]));
+            if (r[2]) { fr.push_back(us(r[3])); lr.push_back(us(r[4])); rounds += (long long)r[2]; workers++; }
+        }
+        auto q = [](std::vector<double> v, double p) {
+            if (v.empty()) return -1.0;
+            std::sort(v.begin(), v.end());
+            return v[(size_t)(p * (double)(v.size() - 1))];
+        };
+        fprintf(stderr, "[pipe] waves %lld | start max %.1f | stage end p50 %.1f p90 %.1f max %.1f | %lld tail rounds on %lld waves "
+                "| first round start min %.1f p50 %.1f max %.1f | last round end p50 %.1f max %.1f | exit max %.1f us\n",
+                (long long)waves, q(st, 1.0), q(se, 0.5), q(se, 0.9), q(se, 1.0), rounds, workers, q(fr, 0.0), q(fr, 0.5),
+                q(fr, 1.0), q(lr, 0.5), q(lr, 1.0), q(ex, 1.0));
+    }
     return hipGetLastError();
 }
