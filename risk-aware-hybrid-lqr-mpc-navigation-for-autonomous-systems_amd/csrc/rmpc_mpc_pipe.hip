@@ -59,8 +59,12 @@ __device__ __forceinline__ int rlx_load(const int32_t *p) {
 //    launch instead of 0.34 ms).
 __device__ __forceinline__ int pipe_claim(const PipeCtl pc, int want) {
     const unsigned waves = gridDim.x;
-    if (!pc.nowait && (unsigned)rlx_load(pc.started) >= waves)
-        return __hip_atomic_fetch_add(pc.head, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!pc.nowait && (unsigned)rlx_load(pc.started) >= waves) {
+        const int h = __hip_atomic_fetch_add(pc.head, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // every stage done and the ticket past the (final) count: leave without waiting
+        if ((unsigned)rlx_load(pc.done) >= waves && h >= rlx_load(pc.count)) return -1;
+        return h;
+    }
     for (;;) {
         const int c = rlx_load(pc.count);
         int hh = rlx_load(pc.head);
@@ -74,12 +78,12 @@ __device__ __forceinline__ int pipe_claim(const PipeCtl pc, int want) {
 // Wait for slot t's stamp.  False when the slot will never be filled: every wave's stage is done
 // (`done` == grid: their hand-ons had completed before they counted, so the count is final) and
 // t is past the count.  The slot's own stamp word is polled (one line per wave's four slots,
-// spread over the chip); the shared `done` word only every 16th poll.  Bounded: 0.2 s.
+// spread over the chip); the shared `done` word every 4th poll.  Bounded: 0.2 s.
 __device__ __forceinline__ bool pipe_wait_slot(const PipeCtl pc, int t) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (unsigned i = 0;; i++) {
         if (__hip_atomic_load(pc.ready + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pc.stamp) return true;
-        if ((i & 15u) == 15u && (unsigned)rlx_load(pc.done) >= gridDim.x) {
+        if ((i & 3u) == 3u && (unsigned)rlx_load(pc.done) >= gridDim.x) {
             if (t >= rlx_load(pc.count)) return false;
         }
         if (__builtin_amdgcn_s_memrealtime() - t0 > RMPC_PIPE_SPIN_TICKS) return false;
