@@ -172,13 +172,6 @@ int rmpc_ctx_set_side_stream(RmpcCtx *ctx, int32_t on);
  * The hybrid step's MPC branch (a different robot subset each step) warm-starts only the robots
  * whose previous solve was the previous call.  Turning it on resets the sets. */
 int rmpc_ctx_set_warm_start(RmpcCtx *ctx, int32_t on);
-/* Pipeline form of the MPC solve on this context (a performance setting; the certified optimum
- * is the same): 0 = stage kernels in sequence (lane-per-robot PDAS stage, then the lane-group
- * tail); 1 = overlapped, both stages in one launch -- every wave of the first stage turns tail
- * consumer when its own robots are done and solves the robots other waves hand on while they
- * still run.  Applies where both stages have an instance of the batch's
- * shape (fp64 LTV, N = 20, 3 obstacles: BASELINE configs 3 and 5); other shapes run in stages. */
-int rmpc_ctx_set_pipeline(RmpcCtx *ctx, int32_t mode);
 int rmpc_mpc_stage_times(RmpcCtx *ctx, double *out3);
 
 /* ---- MPC --------------------------------------------------------------------------------

@@ -119,11 +119,6 @@ struct RmpcCtx {
     // pipeline, the hybrid step's counter pairs, warm-start sets and stamps), which is correct
     // in stream order.  A call on another stream than the previous call's first waits for that
     // call (order_calls): an event recorded at the end of every stateful call (last_ev).
-    // Overlapped pipeline (rmpc_ctx_set_pipeline; rmpc_mpc_pipe.hip): per retry slot, the stamp
-    // of the call that published it (zeroed once at allocation), and this context's call stamp
-    int pipe_mode = 0;
-    DevBuf pipe_ready;
-    uint32_t pipe_stamp = 0;
     hipEvent_t last_ev = nullptr;
     hipStream_t last_s = nullptr;
     bool last_valid = false;
@@ -287,7 +282,6 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     for (auto &e : c->rev)
         if (e) (void)hipEventDestroy(e);
     if (c->last_ev) (void)hipEventDestroy(c->last_ev);
-    c->pipe_ready.release();
     c->retry_r.release();
     c->retry_sets_r.release();
     c->retry2.release();
@@ -361,14 +355,6 @@ int rmpc_ctx_set_warm_start(RmpcCtx *c, int32_t on) {
         sc->warm_on = on != 0;
         sc->warm_B = -1;
     }
-    return RMPC_OK;
-}
-
-int rmpc_ctx_set_pipeline(RmpcCtx *c, int32_t mode) {
-    if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
-    if (mode < 0 || mode > 1) return fail(RMPC_EINVAL, "pipeline mode %d is neither 0 nor 1", mode);
-    c->pipe_mode = mode;
-    for (auto &sc : c->sub) sc->pipe_mode = mode;
     return RMPC_OK;
 }
 
@@ -710,44 +696,6 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
             a.refine = (int32_t *)c->refine.p;
             a.refine_count = cnt + 6;
             a.refine_sets = (uint32_t *)c->refine_sets.p;
-        }
-        // Overlapped pipeline (rmpc_ctx_set_pipeline): the lane-per-robot stage and the lane-group
-        // tail in one launch (rmpc_mpc_pipe.hip); config 3's shape, fp64, one pass
-        const char *pk = rmpc_knob("RMPC_PIPE");
-        const bool pipe = (pk ? atoi(pk) > 0 : c->pipe_mode > 0) && !refine && nsplit == 0 && !prof && warm &&
-                          rmpc_mpc_pipe_supported(p->horizon, bs, prec, lti, n_obs) &&
-                          rmpc_mpc_group_supported(p->horizon, bs, n_obs) && !rmpc_knob("RMPC_DISABLE_DENSE");
-        if (pipe) {
-            const size_t bytes = (size_t)B * sizeof(uint32_t);
-            if (c->pipe_ready.cap < bytes) {
-                HIP_TRY(c->pipe_ready.ensure(bytes));
-                HIP_TRY(hipMemsetAsync(c->pipe_ready.p, 0, c->pipe_ready.cap, s));
-            }
-            if (++c->pipe_stamp == 0) c->pipe_stamp = 1;
-            a.ready = (uint32_t *)c->pipe_ready.p;
-            a.ready_stamp = c->pipe_stamp;
-            HIP_TRY(c->retry2.ensure((size_t)B * sizeof(int32_t)));
-            const int tail_cap = rmpc_knob("RMPC_DENSE_CAP") ? atoi(rmpc_knob("RMPC_DENSE_CAP"))
-                                 : c->tail_cap > 0          ? c->tail_cap
-                                                            : 4;
-            if (c->timing) HIP_TRY(hipEventRecord(c->ev[0], s));
-            HIP_TRY(rmpc_launch_mpc_pipe(a, p->horizon, bs, (int32_t *)c->retry2.p, cnt + 8, tail_cap, cnt + 12, s));
-            if (c->timing) {
-                HIP_TRY(hipEventRecord(c->ev[1], s));
-                HIP_TRY(hipEventRecord(c->ev[2], s));
-            }
-            dbg_sync(s, "pipe");
-            HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
-                                        step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
-                                        c->ws.p, (const int32_t *)c->retry2.p, cnt + 8, s, rmpc_mpc_lds_lanes(L),
-                                        other_counts(c)));
-            if (B > 0) flip_counts(c);
-            if (c->timing) {
-                HIP_TRY(hipEventRecord(c->ev[3], s));
-                c->timed = true;
-            }
-            dbg_sync(s, "generic");
-            return RMPC_OK;
         }
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[0], s));
         {

@@ -1,6 +1,5 @@
-// rmpc_fast_body.h -- the lane-per-robot PDAS stage (fast_body), shared by the stage kernel
-// (rmpc_mpc_fast.hip: mpc_ltv_fast_kernel) and the overlapped pipeline kernel
-// (rmpc_mpc_pipe.hip).  `wid` is the wave's index in the stage (blockIdx.x of the stage kernel).
+// rmpc_fast_body.h -- the lane-per-robot PDAS stage (fast_body), included by the stage kernel
+// (rmpc_mpc_fast.hip: mpc_ltv_fast_kernel).  `wid` is the wave's index in the stage.
 #pragma once
 #include "rmpc_device.h"
 #include "rmpc_internal.h"
@@ -189,9 +188,7 @@ template <> struct Big<float> { static constexpr float v = 1e30f; };
 // WS: the warm start across calls (MpcFastArgs::prev_sets) is compiled in.  Config 3's instance
 // is built both ways and the cold one launched when prev_sets is null: the read and write-back
 // cost its register allocation ~1% (profiles/r03/ab_warm_start.txt).
-// PUB: the overlapped pipeline's instance (rmpc_mpc_pipe.hip) -- retry entries are stored
-// write-through (agent-scope stores) and published with a stamp; no L2 write-back fence
-template <int N, int BS, typename T, bool LTI, int NO = 0, int PR = 1, bool WS = true, bool PUB = false>
+template <int N, int BS, typename T, bool LTI, int NO = 0, int PR = 1, bool WS = true>
 __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
     static_assert(!LTI || BS == 1, "LTI ignores move blocking");
     static_assert(PR == 1 || (PR == 2 && NO > 0 && NO % 2 == 0 && BS == 1 && !LTI && NO / 2 <= 4),
@@ -1022,22 +1019,6 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
             int base = 0;
             if (rank == 0) base = atomicAdd(count, (int)__popcll(m));
             const int slot = __builtin_amdgcn_readfirstlane(base) + rank;
-            if constexpr (PUB) {
-                // overlapped pipeline: the entry and its sets go out write-through (agent-scope
-                // stores reach the device-coherent level without a cache write-back), then,
-                // once they have completed, the call's stamp publishes the slot
-                __hip_atomic_store(list + slot, (int32_t)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                uint32_t *ws = sets + slot;
-#pragma unroll
-                for (int k = 0; k < N; k++) __hip_atomic_store(ws + k * a.B, Hf.get(k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-                for (int j = 0; j < NB; j++)
-                    __hip_atomic_store(ws + (N + j) * a.B, Bf.get(j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(ws + (N + NB) * a.B, (uint32_t)it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(a.ready + slot, a.ready_stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                return;
-            }
             list[slot] = (int32_t)b;
             if (sets) {                                       // ... from this active set
                 // slot-minor record (word w at sets[w * B + slot]): a wave's consecutive

@@ -1,6 +1,5 @@
-// rmpc_group_body.h -- the lane-group tail's solve (group_solve) and its helpers, shared by
-// the tail kernel (rmpc_mpc_group.hip: mpc_group_kernel) and the overlapped pipeline kernel
-// (rmpc_mpc_pipe.hip).
+// rmpc_group_body.h -- the lane-group tail's solve (group_solve) and its helpers, included by
+// the tail kernel (rmpc_mpc_group.hip: mpc_group_kernel).
 #pragma once
 #include "rmpc_device.h"
 #include "rmpc_internal.h"
@@ -344,9 +343,7 @@ __shared__ double grp_junk[64];
 // LTI: MPCController.solve (mpc_controller.py:150-314) -- absolute states tracking the
 // (padded) references, ONE linearisation at the first reference, |u| box, rows on absolute
 // positions; no unwrap, ramp or step count.  Otherwise solve_with_ltv (:345-522).
-// SC1: the overlapped pipeline's consumer (rmpc_mpc_pipe.hip) -- the list entry and its sets
-// were published within the launch and are read with agent-scope loads (no acquire fence)
-template <int N, int BS, int G, typename T, bool LTI, bool SC1 = false>
+template <int N, int BS, int G, typename T, bool LTI>
 __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
                                             int t, bool have, int gl, int grp) {
     constexpr int NB = (N + BS - 1) / BS;
@@ -358,11 +355,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
     const T P0 = p.P[0], P1 = p.P[1], P2 = p.P[2];
     const T eps_h = SetTol<T>::hinge, eps_b = SetTol<T>::box;
     if (a.chk && have && (t < 0 || t >= a.nB)) { diag_hit(a.chk, 8, 2, t); have = false; }
-    auto ld_pub = [&](const auto *p) __attribute__((always_inline)) {
-        if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else return *p;
-    };
-    int64_t b = have ? (int64_t)ld_pub(a.index + t) : 0;
+    int64_t b = have ? (int64_t)a.index[t] : 0;
     if (a.chk && have && (b < 0 || b >= a.nB)) { diag_hit(a.chk, 1, 1, b); b = 0; have = false; }
     GSITE(1);
     const double *xr = a.x_refs + ref_row0(a.prm.ref_off, b, a.ref_rows) * 3;
@@ -513,9 +506,9 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
         // (retry records are slot-minor: word w of list entry t at warm[w * nB + t])
         const uint32_t *ws = (a.warm && have) ? a.warm + t : nullptr;
         const int64_t S = a.nB;
-        for (int k = gl; k < N; k += G) HF(k) = (ws && k > 0) ? ld_pub(ws + k * S) : 0u;
-        for (int j = gl; j < NB; j += G) BF(j) = ws ? ld_pub(ws + (N + j) * S) : 0u;
-        if (ws) it0 = (int)ld_pub(ws + (N + NB) * S);
+        for (int k = gl; k < N; k += G) HF(k) = (ws && k > 0) ? ws[k * S] : 0u;
+        for (int j = gl; j < NB; j += G) BF(j) = ws ? ws[(N + j) * S] : 0u;
+        if (ws) it0 = (int)ws[(N + NB) * S];
     }
     __syncthreads();
 

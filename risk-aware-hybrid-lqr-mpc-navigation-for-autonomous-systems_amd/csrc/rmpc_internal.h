@@ -85,11 +85,6 @@ struct MpcFastArgs {
     uint32_t *prev_sets;
     int prev_shift;
     uint32_t prev_stamp;
-    // Overlapped pipeline (rmpc_mpc_pipe.hip): each retry entry is published by storing
-    // ready_stamp into ready[slot] (agent-scope release) once its robot and sets are written;
-    // null: the stage kernels, no publishing
-    uint32_t *ready;
-    uint32_t ready_stamp;
 };
 // list counters per set of a context (retry_count holds two sets, used by alternate calls)
 #define RMPC_COUNT_WORDS 16
@@ -114,14 +109,6 @@ struct GroupDiag {
 };
 
 bool rmpc_mpc_group_supported(int N, int bs, int no, bool f32 = false);
-// Overlapped pipeline (rmpc_mpc_pipe.hip): the lane-per-robot stage and the lane-group tail in
-// one launch -- each wave runs its robots' PDAS stage, then takes retry entries as they are
-// published until every wave's stage is done and the list is drained.  ctr: three zeroed words
-// (waves started, list head, waves done); ready: per retry slot, the stamp of the call that
-// published it (any contents at first use).
-bool rmpc_mpc_pipe_supported(int N, int bs, int prec, bool lti, int no);
-hipError_t rmpc_launch_mpc_pipe(const MpcFastArgs &a, int N, int bs, int32_t *retry2, int32_t *retry2_count,
-                                int tail_cap, int32_t *ctr, hipStream_t stream);
 hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no, int64_t capacity,
                                  const double *x0, const double *x_refs, int ref_rows,
                                  const double *u_refs, int uref_rows, const double *obstacles,

@@ -241,13 +241,6 @@ def set_side_stream(on=True, device=0, slot=0):
     check(lib.rmpc_ctx_set_side_stream(nat.context(device, slot), int(bool(on))), "rmpc_ctx_set_side_stream")
 
 
-def set_pipeline(mode=1, device=0, slot=0):
-    """Pipeline form of the MPC solve on one context (rmpc_ctx_set_pipeline): 0 = stage
-    kernels in sequence, 1 = both stages overlapped in one launch (same optimum)."""
-    lib = nat.load()
-    check(lib.rmpc_ctx_set_pipeline(nat.context(device, slot), int(mode)), "rmpc_ctx_set_pipeline")
-
-
 def set_warm_start(on=True, device=0, slot=0):
     """Warm start across calls on one context (rmpc_ctx_set_warm_start): each whole-batch MPC
     solve starts robot b's active-set iteration from robot b's previous certified sets, shifted
