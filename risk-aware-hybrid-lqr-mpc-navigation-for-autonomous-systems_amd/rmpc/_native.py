@@ -191,7 +191,14 @@ def own_context(device=0):
     belong to that controller).  Release it with release_context."""
     lib = load()
     h = _vp()
-    check(lib.rmpc_ctx_create(int(device), C.byref(h)), "rmpc_ctx_create")
+    key = int(device) if np.ndim(device) == 0 else tuple(int(d) for d in device)
+    if isinstance(key, tuple) and len(key) == 1:
+        key = key[0]
+    if isinstance(key, tuple):                  # a device list: rmpc_ctx_create_multi, as context()
+        ids = (C.c_int32 * len(key))(*key)
+        check(lib.rmpc_ctx_create_multi(ids, len(key), C.byref(h)), "rmpc_ctx_create_multi")
+    else:
+        check(lib.rmpc_ctx_create(key, C.byref(h)), "rmpc_ctx_create")
     return h
 
 

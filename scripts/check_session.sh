@@ -7,7 +7,7 @@ tag=${1:-chk}; rdir=${2:-profiles/r04}
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
     > gpurun_out/suite_$tag.txt 2>&1 || { tail -40 gpurun_out/suite_$tag.txt; exit 1; }
 tail -1 gpurun_out/suite_$tag.txt
-timeout -k 10 700 bash scripts/measure_round.sh $tag $rdir > gpurun_out/${tag}_measure.log 2>&1 || { tail -20 gpurun_out/${tag}_measure.log; exit 1; }
+timeout -k 10 900 bash scripts/measure_round.sh $tag $rdir > gpurun_out/${tag}_measure.log 2>&1 || { tail -20 gpurun_out/${tag}_measure.log; exit 1; }
 tail -5 gpurun_out/${tag}_measure.log | cut -c1-250
 CL_RATE=5 CL_CAPS="3,4;4,4" timeout -k 10 250 python scripts/closed_loop_warm.py 65536 100 1 3 \
     > gpurun_out/${tag}_clw5.out 2> gpurun_out/${tag}_clw5.err || { tail gpurun_out/${tag}_clw5.err; exit 1; }

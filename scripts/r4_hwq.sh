@@ -1,0 +1,10 @@
+#!/bin/bash
+# Batches in flight against the process's hardware queues (GPU_MAX_HW_QUEUES, HIP default 4):
+# config 3 with 3-6 batches in flight at 4 and 8 queues
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
+STEPS=60 bash scripts/ab.sh "" "-" "GPU_MAX_HW_QUEUES=8" || exit 1
+STEPS=60 bash scripts/ab.sh "--inflight 4" "-" "GPU_MAX_HW_QUEUES=8" || exit 1
+STEPS=60 bash scripts/ab.sh "--inflight 6" "GPU_MAX_HW_QUEUES=8" || exit 1
+STEPS=60 bash scripts/ab.sh "--inflight 8" "GPU_MAX_HW_QUEUES=8" || exit 1
+STEPS=20 bash scripts/ab.sh "" "-" "GPU_MAX_HW_QUEUES=8" || exit 1
+STEPS=20 bash scripts/ab.sh "--inflight 6" "GPU_MAX_HW_QUEUES=8" || exit 1
