@@ -76,6 +76,11 @@ struct RmpcCtx {
     hipStream_t stream = nullptr;
     DevBuf ws;                 // solver workspace
     DevBuf stage[SB_COUNT];    // staging buffers for host-pointer entry points
+    // small host-array MPC calls (rmpc_mpc_solve_batch, <= RMPC_PACK_MAX bytes): every array
+    // packed into one pinned host block and one device block, one copy each way
+    void *pin = nullptr;
+    size_t pin_cap = 0;
+    DevBuf pack;
     DevBuf idx_lqr, idx_mpc, counts, hyb_status;
     DevBuf fast_gains, retry, retry2, retry_count, prof, retry_sets;
     DevBuf retry_a, retry_sets_a, retry_b, retry_sets_b;   // multi-pass fast stage: ping-pong lists and sets
@@ -192,6 +197,7 @@ static int multi_run(RmpcCtx *c, int64_t B, std::vector<RowArr> arrs, F fn) {
 
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+#define RMPC_PACK_MAX ((size_t)256 << 10)   // bytes: the packed host-array path (rmpc_mpc_solve_batch)
 
 extern "C" {
 
@@ -265,6 +271,9 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->ws.release();
     for (auto &b : c->stage) b.release();
+    c->pack.release();
+    if (c->pin) (void)hipHostFree(c->pin);
+    c->pin = nullptr;
     c->idx_lqr.release();
     c->idx_mpc.release();
     c->counts.release();
@@ -958,6 +967,53 @@ extern "C" int rmpc_mpc_solve_batch(RmpcCtx *c, const RmpcMpcParams *p, int64_t 
                          });
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipSetDevice(c->device));
+    {
+        // Small batches (a drop-in MPCController: one robot per call): one pinned block and one
+        // copy each way instead of a pageable copy per array (thirteen).  Layout: inputs, the
+        // in/out step counts, outputs; absent optional arrays take no room and stay NULL.
+        size_t off = 0;
+        auto at = [&](size_t bytes) { const size_t o = off; off += align_up(bytes, 256); return o; };
+        const size_t o_x0 = at((size_t)B * 24), o_xr = at((size_t)B * ref_rows * 24), o_ur = at((size_t)B * uref_rows * 16),
+                     o_ob = at((size_t)n_obs * 24), o_sc = at(step_count ? (size_t)B * 4 : 0), o_u0 = at((size_t)B * 16),
+                     o_us = at(u_seq ? (size_t)B * N * 16 : 0), o_xp = at(x_pred ? (size_t)B * (N + 1) * 24 : 0),
+                     o_co = at(cost ? (size_t)B * 8 : 0), o_st = at((size_t)B * 4), o_sl = at(slack_used ? (size_t)B : 0),
+                     o_it = at(iters ? (size_t)B * 4 : 0);
+        if (off <= RMPC_PACK_MAX) {
+            if (c->pin_cap < off) {
+                if (c->pin) (void)hipHostFree(c->pin);
+                c->pin = nullptr;
+                c->pin_cap = 0;
+                HIP_TRY(hipHostMalloc(&c->pin, align_up(off, 65536), hipHostMallocDefault));
+                c->pin_cap = align_up(off, 65536);
+            }
+            HIP_TRY(c->pack.ensure(off));
+            char *h = (char *)c->pin, *d = (char *)c->pack.p;
+            memcpy(h + o_x0, x0, (size_t)B * 24);
+            memcpy(h + o_xr, x_refs, (size_t)B * ref_rows * 24);
+            memcpy(h + o_ur, u_refs, (size_t)B * uref_rows * 16);
+            if (n_obs > 0) memcpy(h + o_ob, obstacles, (size_t)n_obs * 24);
+            if (step_count) memcpy(h + o_sc, step_count, (size_t)B * 4);
+            HIP_TRY(hipMemcpyAsync(d, h, o_u0, hipMemcpyHostToDevice, own(c)));
+            auto dp = [&](const void *user, size_t o) { return user ? (void *)(d + o) : nullptr; };
+            RC(rmpc_mpc_solve_batch_dev(c, p, B, (const double *)(d + o_x0), (const double *)(d + o_xr), ref_rows,
+                                        (const double *)(d + o_ur), uref_rows, n_obs > 0 ? (const double *)(d + o_ob) : nullptr,
+                                        n_obs, (int32_t *)dp(step_count, o_sc), (double *)(d + o_u0),
+                                        (double *)dp(u_seq, o_us), (double *)dp(x_pred, o_xp), (double *)dp(cost, o_co),
+                                        (int32_t *)(d + o_st), (uint8_t *)dp(slack_used, o_sl), (int32_t *)dp(iters, o_it),
+                                        own(c)));
+            HIP_TRY(hipMemcpyAsync(h + o_sc, d + o_sc, off - o_sc, hipMemcpyDeviceToHost, own(c)));
+            HIP_TRY(hipStreamSynchronize(own(c)));
+            if (step_count) memcpy(step_count, h + o_sc, (size_t)B * 4);
+            memcpy(u0, h + o_u0, (size_t)B * 16);
+            if (u_seq) memcpy(u_seq, h + o_us, (size_t)B * N * 16);
+            if (x_pred) memcpy(x_pred, h + o_xp, (size_t)B * (N + 1) * 24);
+            if (cost) memcpy(cost, h + o_co, (size_t)B * 8);
+            memcpy(status, h + o_st, (size_t)B * 4);
+            if (slack_used) memcpy(slack_used, h + o_sl, (size_t)B);
+            if (iters) memcpy(iters, h + o_it, (size_t)B * 4);
+            return RMPC_OK;
+        }
+    }
     double *dx0, *dxr, *dur, *dobs = nullptr, *du0, *duseq, *dxp, *dcost;
     int32_t *dstep, *dst, *dit;
     uint8_t *dsl;
