@@ -714,7 +714,7 @@ def drop_in_latency(local, n_calls=200, skip=10):
         xr_all, ur_all = rmpc.batch.figure8_batch(np.arange(n_calls) * 0.02, N + 1, device=local)
         x = xr_all[0, 0] + np.array([0.05, -0.05, 0.1])
         obs = [rmpc.Obstacle(*o) for o in W.DEFAULT_OBS]
-        ts, rep, its, seq = [], [], [], []
+        ts, rep, its, seq, nonopt = [], [], [], [], 0
         for k in range(n_calls):
             t = time.perf_counter()
             s = c.solve_with_ltv(x, xr_all[k], ur_all[k], obs)
@@ -722,12 +722,12 @@ def drop_in_latency(local, n_calls=200, skip=10):
             rep.append(s.solve_time_ms)
             its.append(s.iterations)
             seq.append(x.copy())
-            assert s.status == "optimal"
+            nonopt += s.status != "optimal"
             x = rmpc.batch.plant_step_batch(x[None], s.optimal_control[None], 0.02, 2.0, 3.0, device=local)[0]
         us = np.asarray(ts[skip:]) * 1e6
         res[f"N{N}_bs{bs}"] = {"median_us": float(np.median(us)), "p90_us": float(np.percentile(us, 90)),
                                "solve_time_ms_median": float(np.median(rep[skip:])),
-                               "iters_mean": float(np.mean(its[skip:])), "calls": n_calls - skip,
+                               "iters_mean": float(np.mean(its[skip:])), "calls": n_calls - skip, "not_optimal": nonopt,
                                "vs_reference_logged_mean": REF_LOGGED_SOLVE_MS * 1e3 / float(np.median(us))}
         seqs[(N, bs)] = (np.asarray(seq), xr_all, ur_all)
     res["reference_logged_mean_ms"] = REF_LOGGED_SOLVE_MS

@@ -4,10 +4,10 @@
 # Usage: bash scripts/gpurun_submit.sh <log> <timeout s> '<command>'
 log=$1; to=$2; cmd=$3
 cd /root/repo
-for i in $(seq 1 12); do
+for i in $(seq 1 40); do
   /usr/local/graft/bin/gpurun --timeout "$to" -- "$cmd" > "$log" 2>&1
   st=$(python3 -c "import json;print(json.load(open('gpurun_out/.last_call.json')).get('status'))" 2>/dev/null)
   run=$(python3 -c "import json;print(json.load(open('gpurun_out/.last_call.json')).get('run_s') or 0)" 2>/dev/null)
   if [ "$st" != "transient" ] || [ "$run" != "0.0" -a "$run" != "0" ]; then exit 0; fi
-  sleep 90
+  sleep 150
 done
