@@ -13,7 +13,7 @@ step() { echo "== $(date +%T) $*"; }
 prof() {   # prof <name> <bench args...>: rocprofv3 kernel trace + stats of a short bench run
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof_$name -o run --output-format csv \
-    -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pcie --no-closed-loop "$@" \
+    -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pcie --no-closed-loop --no-drop-in "$@" \
     > gpurun_out/${tag}_prof_${name}_bench.json 2> gpurun_out/${tag}_prof_$name.err || { tail gpurun_out/${tag}_prof_$name.err; exit 1; }
 }
 # PMC passes per configuration (entry kernel = the first kernel of each library call); the

@@ -13,3 +13,7 @@ STEPS=30 bash scripts/ab.sh "--config cfg4 --inflight 1" "-" || exit 1
 for c in 8,6 10,6 10,8 12,8 16,6; do
   STEPS=30 bash scripts/ab.sh "--config cfg4 --inflight 1 --stage-caps $c" "-" || exit 1
 done
+# clean rocprofv3 kernel statistics of one config-3 batch (no drop-in calls in the run)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r4h_prof_cfg3_inflight1 -o run --output-format csv \
+  -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pcie --no-closed-loop --no-drop-in --inflight 1 \
+  > gpurun_out/r4h_prof_cfg3_inflight1_bench.json 2> gpurun_out/r4h_prof.err || exit 1
