@@ -199,6 +199,28 @@ def parallelism(args, world):
     return s
 
 
+def alone_times(run_one, stream, K, skip=2):
+    """One batch at a time on one stream: (ms per launch for K launches back to back between two
+    HIP events -- a single fleet's rate, the roofline's launch time -- and the mean ms of K more
+    launches each between its own pair of events, whose packets sit between the launches)."""
+    import numpy as np
+    import torch
+    for _ in range(skip):
+        run_one()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for _ in range(K):
+        run_one()
+    b.record(stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    for e0, e1 in ev:
+        e0.record(stream)
+        run_one()
+        e1.record(stream)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / K, float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
+
+
 def timed_loop(step, steps, warmup, dist, sync, S=1):
     """The timing contract: max(W, S) untimed steps, then exactly K steps (step k on in-flight
     slot k mod S) bracketed by barrier + synchronize on both sides.  Returns this rank's
@@ -432,30 +454,17 @@ def main():
     # inputs, outputs and step counters were written on the default stream: the other
     # streams start only after that work (they are non-blocking streams)
     elapsed = timed_loop(step, args.steps, args.warmup, dist, torch.cuda.synchronize, S)
-    # one batch's launch on its own (HIP events on the launch stream, no other batch in
-    # flight): the roofline's kernel time
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        step()
-        ev[i][1].record(stream)
-    torch.cuda.synchronize()
-    k_ms = [a.elapsed_time(b) for a, b in ev]
-    k_avg_s = float(np.mean(k_ms)) / 1e3
+    # one batch's launches on their own (nothing else in flight; HIP events on the launch
+    # stream): the roofline's launch time
+    k_ms, k_evt_ms = alone_times(lambda: step(0), stream, args.steps)
+    k_avg_s = k_ms / 1e3
     # ... and with the library's default stage caps on a context of its own (what one batch at
     # a time would use; its side stream on, rmpc_ctx_set_side_stream)
     if caps[0]:
         rmpc.batch.set_stage_caps(0, 0, device=local, slot=S)
-        ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.steps + 2)]
-        for i in range(args.steps + 2):
-            ev2[i][0].record(stream)
-            rmpc.batch.mpc_solve_batch_dev(p, x0, xr, ur, obs, outs[0], step_count=counts_sc[0],
-                                           device=local, stream=stream, slot=S)
-            ev2[i][1].record(stream)
-        torch.cuda.synchronize()
-        alone_default_s = float(np.mean([a.elapsed_time(b) for a, b in ev2[2:]])) / 1e3
+        alone_default_s = alone_times(lambda: rmpc.batch.mpc_solve_batch_dev(
+            p, x0, xr, ur, obs, outs[0], step_count=counts_sc[0], device=local, stream=stream, slot=S),
+            stream, args.steps)[0] / 1e3
     if alone_default_s is None or not caps[0]:
         alone_default_s = k_avg_s
 
@@ -535,6 +544,8 @@ def main():
                      "pipe": pipe,
                      "kernel": f"MPC launch: {fast_name} -> {tail_name} -> mpc_solve_kernel",
                      "kernel_avg_ms": k_avg_s * 1e3,
+                     "kernel_avg_ms_note": "K launches back to back on one stream between two HIP events",
+                     "launch_ms_own_events": k_evt_ms,
                      "stage_ms": None if stage_ms is None else {
                          fast_name: stage_ms[0], tail_name: stage_ms[1],
                          "mpc_solve_kernel": stage_ms[2]},
@@ -819,19 +830,12 @@ def closed_loop(dev, B, obs_list, N=20, f32=False, K=50, fleets_max=3, hybrid=Fa
 
 def _timed(args, step, dist, dev, S=1):
     """W warm-up steps, then K steps between barrier + synchronize, step k on in-flight slot
-    k mod S; then K single-slot steps bracketed by HIP events on the launch stream (one batch's
-    own device time).  Returns (elapsed s, event ms list)."""
+    k mod S; then one batch alone on the launch stream (alone_times).  Returns (elapsed s,
+    (ms per launch back to back, ms per launch between its own events))."""
     import torch
     stream = torch.cuda.current_stream()
     elapsed = timed_loop(step, args.steps, args.warmup, dist, torch.cuda.synchronize, S)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        step(0)
-        ev[i][1].record(stream)
-    torch.cuda.synchronize()
-    return elapsed, [a.elapsed_time(b) for a, b in ev]
+    return elapsed, alone_times(lambda: step(0), stream, args.steps)
 
 
 def _scipy_lqr_chunk(args):
@@ -971,22 +975,14 @@ def bench_other(args, world, rank, local, dist, pre=None):
         flops_unit, bytes_unit = None, None
         workload = (f"cfg5: run_hybrid_simulation step, N={N}, 3 obstacles, ~50% of robots within "
                     f"0.767 m of an obstacle edge, {B_per} robots/GPU")
-    elapsed, k_ms = _timed(args, step, dist, dev, S)
-    k_avg_s = float(np.mean(k_ms)) / 1e3
+    elapsed, (k_ms, k_evt_ms) = _timed(args, step, dist, dev, S)
+    k_avg_s = k_ms / 1e3
     alone_default_s = None
     if args.config == "cfg5" and caps[0]:
         # one batch alone with the library's default caps (what one batch at a time would use)
         torch.cuda.synchronize()
         rmpc.batch.set_stage_caps(0, 0, device=local, slot=0)
-        stream0 = torch.cuda.current_stream()
-        ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.steps + 2)]
-        for a, b in ev2:
-            a.record(stream0)
-            step(0)
-            b.record(stream0)
-        torch.cuda.synchronize()
-        alone_default_s = float(np.mean([a.elapsed_time(b) for a, b in ev2[2:]])) / 1e3
+        alone_default_s = alone_times(lambda: step(0), torch.cuda.current_stream(), args.steps)[0] / 1e3
         rmpc.batch.set_stage_caps(*caps, device=local, slot=0)
     elapsed, _ = W.aggregate(dist, elapsed, [], device=coll_device(args, dev))
     line = {"metric": metric, "value": B_total * args.steps / elapsed,
