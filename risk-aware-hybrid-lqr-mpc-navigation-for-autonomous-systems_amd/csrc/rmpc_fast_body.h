@@ -511,6 +511,16 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
 #define RMPC_GLDS 2
 #endif
     constexpr int GLDS = (GREG > 0 && GREG + RMPC_GLDS <= NB) ? RMPC_GLDS : 0;
+    // Diagnostics builds only (scripts/build_variant.sh), both wrong by construction:
+    // RMPC_GAIN_NOMEM drops the tile traffic of the blocks beyond GREG + GLDS (the forward sweep
+    // reads block 0's gains there), RMPC_NOCERT runs every robot to the stage's cap and drops
+    // its outputs -- together the upper bound of what removing the tile traffic could save.
+#ifndef RMPC_GAIN_NOMEM
+#define RMPC_GAIN_NOMEM 0
+#endif
+#ifndef RMPC_NOCERT
+#define RMPC_NOCERT 0
+#endif
     static_assert(GLDS * 8 * RMPC_WAVE * sizeof(T) <= RMPC_WAVE * 17 * sizeof(double), "LDS gain blocks exceed the scratch");
     struct alignas(2 * sizeof(T)) GPair { T x, y; };
     GPair *const glds = reinterpret_cast<GPair *>(lds_raw + (size_t)3 * N * LW * sizeof(T) / sizeof(double)) + lane;
@@ -524,6 +534,9 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
                 const GPair v = glds[((j - GREG) * 4 + q) * RMPC_WAVE];
                 dst[2 * q] = v.x; dst[2 * q + 1] = v.y;
             }
+        } else if constexpr (RMPC_GAIN_NOMEM && GREG > 0) {   // (diagnostics: no tile traffic)
+#pragma unroll
+            for (int q = 0; q < 8; q++) dst[q] = greg[0][q];
         } else if constexpr (PR == 2) gt.ld_pair(j, dst, pp);
         else gt.ld(j, dst);
     };
@@ -698,6 +711,9 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
             } else if (j < GREG + GLDS) {
 #pragma unroll
                 for (int q = 0; q < 4; q++) glds[((j - GREG) * 4 + q) * RMPC_WAVE] = GPair{G[2 * q], G[2 * q + 1]};
+            } else if constexpr (RMPC_GAIN_NOMEM && GREG > 0) {
+#pragma unroll
+                for (int q = 0; q < 8; q++) asm volatile("" ::"v"(G[q]));
             } else if constexpr (PR == 2) gt.st_half(j, G, pp);
             else gt.st(j, G);
 #ifndef RMPC_BSB
@@ -937,6 +953,10 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
             used |= (int)pair_xchg((uint32_t)used);
         }
         if (a.prof) tp_f += __builtin_amdgcn_s_memtime() - tp0;
+        if constexpr (RMPC_NOCERT) {
+            asm volatile("" ::"v"(J), "v"(changed), "v"(used));
+            continue;
+        }
         if (!changed) { cert = 1; break; }
         // PDAS cycling: a repeated active-set signature hands the robot to the
         // projected-Newton phase of the next stage
@@ -965,6 +985,7 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
             atomicAdd(a.prof + 56 + (mi < 7ull ? mi : 7ull), 1ull);     // waves per loop count
         }
     }
+    if constexpr (RMPC_NOCERT) return;
     // The output pass's loads are issued here, before the hand-off's record stores of this
     // wave's other lanes, for the same vmcnt reason (below); not in an fp32 pass that hands
     // every certified robot to the refinement pass (it writes no outputs)
