@@ -15,6 +15,11 @@ for v in nocert nocert_nomem; do
   RMPC_DIAG=1 RMPC_LIB_PATH=$L/librmpc_$v.so timeout -k 10 200 python3 bench.py $B > gpurun_out/gt/${v}_inflight.json \
       2> gpurun_out/gt/${v}_inflight.err || exit 1
 done
+# per-call stream-order event recorded only when a context changes streams (RMPC_LAZY_ORDER)
+STEPS=50 timeout -k 10 500 bash scripts/ab.sh "--inflight 1" - "RMPC_LIB_PATH=$L/librmpc_lazy.so" - "RMPC_LIB_PATH=$L/librmpc_lazy.so" \
+    > gpurun_out/gt/lazy_ab.txt 2>&1 || exit 1
+STEPS=50 timeout -k 10 500 bash scripts/ab.sh "" - "RMPC_LIB_PATH=$L/librmpc_lazy.so" >> gpurun_out/gt/lazy_ab.txt 2>&1 || exit 1
+cat gpurun_out/gt/lazy_ab.txt | cut -c1-200
 timeout -k 10 400 python3 bench.py > gpurun_out/gt/default.json 2> gpurun_out/gt/default.err || exit 1
 python3 - <<'EOF'
 import csv, glob, json
