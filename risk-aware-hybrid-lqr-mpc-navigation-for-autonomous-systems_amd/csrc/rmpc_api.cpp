@@ -467,27 +467,11 @@ static hipError_t side_stream(RmpcCtx *c) {
 
 // Stream order between consecutive stateful calls of one context (RmpcCtx::last_ev): a call
 // on another stream than the previous one waits for the previous call's end on the device.
-#ifndef RMPC_LAZY_ORDER
-#define RMPC_LAZY_ORDER 0   // (A/B: record the previous stream's event only when the stream changes)
-#endif
 static hipError_t order_calls(RmpcCtx *c, hipStream_t s) {
-    if (RMPC_LAZY_ORDER && c->last_valid && c->last_s != s) {
-        if (!c->last_ev) {
-            const hipError_t e = hipEventCreateWithFlags(&c->last_ev, hipEventDisableTiming);
-            if (e != hipSuccess) { c->last_ev = nullptr; return e; }
-        }
-        const hipError_t e = hipEventRecord(c->last_ev, c->last_s);
-        if (e != hipSuccess) return e;
-    }
     if (c->last_valid && c->last_s != s) return hipStreamWaitEvent(s, c->last_ev, 0);
     return hipSuccess;
 }
 static hipError_t mark_call(RmpcCtx *c, hipStream_t s) {
-    if (RMPC_LAZY_ORDER) {
-        c->last_valid = true;
-        c->last_s = s;
-        return hipSuccess;
-    }
     if (!c->last_ev) {
         const hipError_t e = hipEventCreateWithFlags(&c->last_ev, hipEventDisableTiming);
         if (e != hipSuccess) { c->last_ev = nullptr; return e; }
