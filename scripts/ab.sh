@@ -20,7 +20,7 @@ import json;d=json.load(open('gpurun_out/ab_$tag.json'));r=d.get('roofline',{})
 print('[$args | $v] value %.4e alone %.4e ms/step %.4f'%(d['value'],d.get('value_one_batch_alone',0),d['ms_per_step']),
       {k: round(x, 4) for k, x in (r.get('stage_ms') or {}).items()}, d.get('solver'), 'du', d.get('max_abs_du_vs_cpu_port'))"
   if [ -n "$PROF" ]; then
-    env $v RMPC_DENSE_PROF=1 timeout -k 10 200 python bench.py $args --inflight 1 --steps 2 --warmup 1 --no-cpu-baseline \
+    env $v RMPC_DENSE_PROF=1 timeout -k 10 200 python bench.py $args --inflight 1 --steps 2 --warmup 1 --no-cpu-baseline --no-closed-loop --no-drop-in \
         --no-pcie > /dev/null 2> gpurun_out/ab_${tag}_prof.err || exit 1
     grep "\[group\]\|\[fast\]\|\[dense\]\|\[refine\]" gpurun_out/ab_${tag}_prof.err | tail -5
   fi
