@@ -1,8 +1,9 @@
 #!/bin/bash
 # A/B: the N = 20 lane-group tail with 32 lanes per robot (two robots per wave) against 16
-# (build: bash scripts/build_variant.sh g32 -DRMPC_TAIL_G20=32 on the tree of the commit that adds this
-# script; the knob was removed after the A/B, profiles/r04/ab_tail_32_lanes.txt).  Parity first (the full-size
-# config-3 and tail-only tests through the variant library), then the bench lines.
+# (a local A/B build, not committed: group_lanes() returning 32 at N = 20 and the N = 20 tail
+# instances built with G = 32, as bash scripts/build_variant.sh g32 -DRMPC_TAIL_G20=32; result in
+# profiles/r04/ab_tail_32_lanes.txt).  Parity first (the full-size config-3 and tail-only tests
+# through the variant library), then the bench lines.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 L=$PWD/risk-aware-hybrid-lqr-mpc-navigation-for-autonomous-systems_amd/rmpc
 RMPC_LIB_PATH=$L/librmpc_g32.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
