@@ -468,8 +468,12 @@ def main():
     if alone_default_s is None or not caps[0]:
         alone_default_s = k_avg_s
 
-    # per-stage device time (separate, untimed pass: events between the pipeline's kernels)
-    # (only the lane-per-robot pipeline has stages; fp32 / other horizons run one kernel)
+    # the roofline prices one batch alone at the library's defaults: the launch the rocprofv3
+    # one-batch statistics and the PMC passes (bench.py --inflight 1) see
+    k_roof_s = alone_default_s
+    # per-stage device time of that launch (separate, untimed pass: events between the
+    # pipeline's kernels; only the lane-per-robot pipeline has stages)
+    rmpc.batch.set_stage_caps(0, 0, device=local, slot=0)
     rmpc.batch.set_stage_timing(True, device=local)
     stage = []
     try:
@@ -480,6 +484,7 @@ def main():
     except rmpc.RmpcError:
         stage_ms = None
     rmpc.batch.set_stage_timing(False, device=local)
+    rmpc.batch.set_stage_caps(*caps, device=local, slot=0)
 
     # N > 1: the same K steps again with the batch gather of u0 inside the timed region
     # (SURVEY 8(e)'s collective: RCCL all_gather over xGMI; the round-robin shards interleave
@@ -511,13 +516,13 @@ def main():
     flops = canonical_flops(N, n_obs, float(its.mean()))
     kflops = kernel_flops(N, n_obs, float(its.mean()))
     abytes = algorithmic_bytes(N, n_obs)
-    achieved = flops * B / k_avg_s / 1e12
+    achieved = flops * B / k_roof_s / 1e12
     line = {
         "metric": "MPC QP solves/sec (N=20, nx=3, nu=2) at 1/2/4/8 MI355X; max |u-u_ref|",
         "value": B_total * args.steps / elapsed,
         # the same batch with nothing else in flight (launches back to back between two HIP
-        # events): with the library's defaults, what one batch at a time runs, and with the
-        # in-flight stage caps, the launch the roofline and the PMC passes price
+        # events): with the library's defaults, what one batch at a time runs (the roofline's
+        # launch), and with the in-flight stage caps
         "value_one_batch_alone": B_total / alone_default_s,
         "value_one_batch_alone_inflight_caps": B_total / k_avg_s,
         "unit": "solves/s",
@@ -544,20 +549,21 @@ def main():
                      "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
                      "pipe": pipe,
                      "kernel": f"MPC launch: {fast_name} -> {tail_name} -> mpc_solve_kernel",
-                     "kernel_avg_ms": k_avg_s * 1e3,
-                     "kernel_avg_ms_note": "one batch alone with the in-flight stage caps (value_one_batch_alone_inflight_caps): K launches back to back on one stream between two HIP events",
-                     "launch_ms_own_events": k_evt_ms,
+                     "kernel_avg_ms": k_roof_s * 1e3,
+                     "kernel_avg_ms_note": "one batch alone at the library's default stage caps (value_one_batch_alone): K launches back to back on one stream between two HIP events",
+                     "inflight_caps_launch_ms": k_avg_s * 1e3,
+                     "inflight_caps_launch_ms_own_events": k_evt_ms,
                      "stage_ms": None if stage_ms is None else {
                          fast_name: stage_ms[0], tail_name: stage_ms[1],
                          "mpc_solve_kernel": stage_ms[2]},
                      "flops_per_solve_canonical": flops,
                      "flops_per_solve_executed": kflops,
-                     "executed_tflops": kflops * B / k_avg_s / 1e12,
+                     "executed_tflops": kflops * B / k_roof_s / 1e12,
                      "algorithmic_bytes_per_solve": abytes,
-                     "hbm_gbs_algorithmic": abytes * B / k_avg_s / 1e9,
-                     "hbm_frac": abytes * B / k_avg_s / 1e9 / HBM_PEAK_GBS,
-                     # kernel_avg_ms / achieved / frac: one batch's launch alone (in-flight
-                     # caps, nothing else in flight); the job's own rate with S batches in flight:
+                     "hbm_gbs_algorithmic": abytes * B / k_roof_s / 1e9,
+                     "hbm_frac": abytes * B / k_roof_s / 1e9 / HBM_PEAK_GBS,
+                     # kernel_avg_ms / achieved / frac: one batch's launch alone (library
+                     # defaults, nothing else in flight); the job's own rate with S batches in flight:
                      "achieved_in_flight": flops * B_total * args.steps / elapsed / world / 1e12,
                      "frac_in_flight": flops * B_total * args.steps / elapsed / world / 1e12 / peak},
         "solver": stats,
@@ -672,7 +678,7 @@ def main():
     # HBM traffic and executed flops per launch from the committed PMC passes of this workload
     # (rocprofv3 --pmc, separate passes; scripts/pmc_hbm.sh, scripts/pmc_flops.sh)
     if not args.lti and not args.f32 and not args.f64 and args.config in ("cfg3", "cfg4"):
-        pmc_into_roofline(line["roofline"], "" if args.config == "cfg3" else "_" + args.config, abytes * B, k_avg_s)
+        pmc_into_roofline(line["roofline"], "" if args.config == "cfg3" else "_" + args.config, abytes * B, k_roof_s)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
@@ -985,6 +991,7 @@ def bench_other(args, world, rank, local, dist, pre=None):
         rmpc.batch.set_stage_caps(0, 0, device=local, slot=0)
         alone_default_s = alone_times(lambda: step(0), torch.cuda.current_stream(), args.steps)[0] / 1e3
         rmpc.batch.set_stage_caps(*caps, device=local, slot=0)
+    k_roof_s = alone_default_s or k_avg_s     # the roofline's launch: one batch alone, library defaults
     elapsed, _ = W.aggregate(dist, elapsed, [], device=coll_device(args, dev))
     line = {"metric": metric, "value": B_total * args.steps / elapsed,
             "value_one_batch_alone": B_total / (alone_default_s or k_avg_s), "unit": unit, "n_gpus": world,
@@ -997,18 +1004,18 @@ def bench_other(args, world, rank, local, dist, pre=None):
     if args.config == "cfg5":
         line["config"]["stage_caps"] = list(caps) if caps[0] else "library default"
     if flops_unit:
-        ach = flops_unit * B / k_avg_s / 1e12
+        ach = flops_unit * B / k_roof_s / 1e12
         line["roofline"] = {"bound": "valu-fp64", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                             "frac": ach / FP64_PEAK_TFLOPS, "traffic": None,
-                            "kernel": "lqr_control_kernel", "kernel_avg_ms": k_avg_s * 1e3,
+                            "kernel": "lqr_control_kernel", "kernel_avg_ms": k_roof_s * 1e3,
                             "flops_per_unit": flops_unit, "algorithmic_bytes_per_unit": bytes_unit,
-                            "hbm_gbs_algorithmic": bytes_unit * B / k_avg_s / 1e9,
+                            "hbm_gbs_algorithmic": bytes_unit * B / k_roof_s / 1e9,
                             "note": "launch-latency bound at this batch (one ~10-15 us kernel)"}
     else:
         used_h = used.cpu().numpy().astype(bool)
         fm = float(used_h.mean())
         line["mpc_fraction"] = fm
-        line["kernel_avg_ms"] = k_avg_s * 1e3
+        line["kernel_avg_ms"] = k_roof_s * 1e3
         # closed loop (rank 0, N=1; never `value`): run_simulation.py's hybrid loop on the device,
         # cold and with the warm start across calls (the MPC branch's robots, per-robot stamps)
         if world == 1 and rank == 0 and not args.no_closed_loop:
@@ -1027,16 +1034,16 @@ def bench_other(args, world, rank, local, dist, pre=None):
         except Exception:   # noqa: BLE001  (diagnostic only)
             its_mpc = 2.2
         f_unit = 10 * 3 + fm * canonical_flops(N, 3, its_mpc) + (1 - fm) * 6.0e3
-        ach = f_unit * B / k_avg_s / 1e12
+        ach = f_unit * B / k_roof_s / 1e12
         line["roofline"] = {"bound": "valu-fp64", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                             "frac": ach / FP64_PEAK_TFLOPS, "traffic": None,
                             "kernel": "hybrid_decide_kernel + lqr_control_kernel + MPC pipeline (compacted lists)",
-                            "kernel_avg_ms": k_avg_s * 1e3, "flops_per_unit_canonical": f_unit,
+                            "kernel_avg_ms": k_roof_s * 1e3, "flops_per_unit_canonical": f_unit,
                             "mpc_iters_mean": its_mpc,
                             "hbm_gbs_algorithmic": (24 + fm * algorithmic_bytes(N, 3, False) + (1 - fm) * 80) * B
-                            / k_avg_s / 1e9}
+                            / k_roof_s / 1e9}
         pmc_into_roofline(line["roofline"], "_cfg5", (24 + fm * algorithmic_bytes(N, 3, False) + (1 - fm) * 80) * B,
-                          k_avg_s)
+                          k_roof_s)
     # ---- CPU baseline (rank 0, N=1): the oracle's C restatement of the same step
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         from oracle import cpu

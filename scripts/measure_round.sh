@@ -27,7 +27,7 @@ pmc() {   # pmc <suffix> <entry kernel> <bench args...>
   bash scripts/pmc_flops.sh ${tag}_fl$sfx "$entry" "$@" > gpurun_out/${tag}_pmc_flops$sfx.log 2>&1 || { tail gpurun_out/${tag}_pmc_flops$sfx.log; exit 1; }
   cp gpurun_out/${tag}_fl${sfx}_flops.json $rdir/pmc_flops$sfx.json
 }
-pmc "" mpc_ltv_fast_kernel
+pmc "" mpc_ltv_fast_kernel --inflight 1
 pmc _cfg4 "mpc_ltv_fast_kernel<30, 1, float" --config cfg4 --inflight 1
 pmc _cfg5 hybrid_decide_kernel --config cfg5 --inflight 1
 step bench cfg3
