@@ -378,6 +378,37 @@ void rmpc_cpu_set_pdas_caps(int fast_cap, int tail_cap) { g_fast_cap = fast_cap;
            /* diagnostics: phase-2 entries, phase-2 iterations, F evaluations */
 long rmpc_cpu_counter(int i) { return (i >= 0 && i < 4) ? g_cnt[i] : 0; }
 void rmpc_cpu_reset_counters(void) { memset(g_cnt, 0, sizeof(g_cnt)); }
+#ifndef RMPC_LS_STUDY
+#define RMPC_LS_STUDY 0
+#endif
+#if RMPC_LS_STUDY > 0
+/* trial step lengths of the study modes: 1 = {1, 1/2, 1/4, 1/8}, 2 = {2, 1, 1/2, 1/4},
+ * 3 = {1.5, 1, 0.7, 0.45}, 4 = 200 points on (0, 2] (the ceiling) */
+static int ls_study_pick(const Prob *pr, double z[NM][2], const Sol *s, double g[NM][2], double F,
+                         double zbest[NM][2], double xbest[NM + 1][3], double *Fbest) {
+    static const double a1[] = {1, .5, .25, .125}, a2[] = {2, 1, .5, .25}, a3[] = {1.5, 1, .7, .45};
+    const int mode = RMPC_LS_STUDY, n = mode == 4 ? 200 : 4;
+    int found = 0;
+    double zt[NM][2], xt[NM + 1][3];
+    for (int i = 0; i < n; i++) {
+        const double alpha = mode == 1 ? a1[i] : mode == 2 ? a2[i] : mode == 3 ? a3[i] : 2.0 * (i + 1) / n;
+        double gd = 0.0;
+        for (int j = 0; j < pr->nb; j++)
+            for (int c = 0; c < 2; c++) {
+                zt[j][c] = clampd(z[j][c] + alpha * (s->u[j][c] - z[j][c]), pr->lo[j][c], pr->hi[j][c]);
+                gd += g[j][c] * (zt[j][c] - z[j][c]);
+            }
+        const double Ft = simulate_F(pr, (const double(*)[2])zt, xt);
+        if (Ft <= F + 1e-4 * gd && (!found || Ft < *Fbest)) {
+            found = 1;
+            *Fbest = Ft;
+            memcpy(zbest, zt, sizeof(zt));
+            memcpy(xbest, xt, sizeof(xt));
+        }
+    }
+    return found;
+}
+#endif
 static int pdas_solve(const Prob *pr, int max_iter, Sol *s) {
     uint8_t hact[NM][OM];
     uint8_t bfix[NM][2];
@@ -461,6 +492,16 @@ static int pdas_solve(const Prob *pr, int max_iter, Sol *s) {
         /* Armijo backtracking along the projection arc */
         double alpha = 1.0, zt[NM][2], Ft = F;
         int acc = 0;
+#if RMPC_LS_STUDY > 0
+        /* (line-search study builds only, scripts/study_linesearch.py: several trial points
+         * along the arc evaluated up front, the lowest F among those passing Armijo taken) */
+        if (ls_study_pick(pr, z, s, g, F, zt, xt, &Ft)) {
+            memcpy(z, zt, sizeof(z));
+            memcpy(x, xt, sizeof(x));
+            F = Ft;
+            continue;
+        }
+#endif
         for (int ls = 0; ls < 40; ls++) {
             double gd = 0.0;
             for (int j = 0; j < pr->nb; j++)
