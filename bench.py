@@ -968,6 +968,8 @@ def bench_other(args, world, rank, local, dist, pre=None):
         # in flight, the MPC branch's first stage runs longer (scripts/r02_s3_caps_cfg.sh:
         # fast cap 9 against the single-batch default 6)
         caps = (9, 4) if S > 1 else (0, 0)
+        if args.stage_caps:
+            caps = tuple(int(v) for v in args.stage_caps.split(","))
         for i in range(S):
             rmpc.batch.set_stage_caps(*caps, device=local, slot=i)
             # (config 5 keeps its side stream in flight: 398-418M against 233M steps/s without)
