@@ -316,17 +316,34 @@ static void gradient(const Prob *pr, const double u[NM][2], const double x[NM + 
     }
 }
 
+#ifndef RMPC_KMAX_STUDY
+#define RMPC_KMAX_STUDY 0
+#endif
+#if RMPC_KMAX_STUDY
+/* (study builds only, scripts/study_gain_reuse.py: histogram of the last step whose sets a
+ * stage-1 PDAS update changed -- the backward sweep's gains beyond it repeat the last sweep's) */
+static long g_kmax_hist[NM + 2];
+static _Thread_local int g_in_stage1;
+void rmpc_cpu_kmax_hist(long *out) { memcpy(out, g_kmax_hist, sizeof(g_kmax_hist)); }
+void rmpc_cpu_kmax_reset(void) { memset(g_kmax_hist, 0, sizeof(g_kmax_hist)); }
+#endif
 /* PDAS set update from a Riccati solution; returns 1 if any set changed */
 static int update_sets(const Prob *pr, const Sol *s, const double lam[NM][2], uint8_t hact[NM][OM],
                        uint8_t bfix[NM][2]) {
     const double eps_h = 1e-14, eps_b = 1e-13;
     int changed = 0;
+#if RMPC_KMAX_STUDY
+    int kmax = -1;
+#define KMAX_NOTE(k) do { if ((k) > kmax) kmax = (k); } while (0)
+#else
+#define KMAX_NOTE(k) do { } while (0)
+#endif
     for (int k = 1; k < pr->N; k++)
         for (int o = 0; o < pr->no; o++) {
             if (!pr->hk[k][o]) continue;
             double r = pr->hb[k][o] - pr->hn0[k][o] * s->x[k][0] - pr->hn1[k][o] * s->x[k][1];
             uint8_t na = hact[k][o] ? (r > -eps_h) : (r > eps_h);
-            if (na != hact[k][o]) { changed = 1; hact[k][o] = na; }
+            if (na != hact[k][o]) { changed = 1; hact[k][o] = na; KMAX_NOTE(k); }
         }
     for (int j = 0; j < pr->nb; j++)
         for (int c = 0; c < 2; c++) {
@@ -340,8 +357,15 @@ static int update_sets(const Prob *pr, const Sol *s, const double lam[NM][2], ui
             } else {
                 if (lam[j][c] > 0) ns = 0;
             }
-            if (ns != st) { changed = 1; bfix[j][c] = ns; }
+            if (ns != st) { changed = 1; bfix[j][c] = ns; KMAX_NOTE(j * pr->bs); }
         }
+#if RMPC_KMAX_STUDY
+    if (changed && g_in_stage1) {
+#pragma omp atomic
+        g_kmax_hist[kmax + 1]++;
+    }
+#endif
+#undef KMAX_NOTE
     return changed;
 }
 
@@ -424,6 +448,9 @@ static int pdas_solve(const Prob *pr, int max_iter, Sol *s) {
     for (; it < max_iter && it < cap1;) {
         riccati_solve(pr, (const uint8_t(*)[OM])hact, (const uint8_t(*)[2])bfix, s, lam);
         s->iters = ++it;
+#if RMPC_KMAX_STUDY
+        g_in_stage1 = it < cap1;      /* an update that the next stage-1 sweep consumes */
+#endif
         if (!update_sets(pr, s, (const double(*)[2])lam, hact, bfix)) {
             s->converged = 1;
             return 1;

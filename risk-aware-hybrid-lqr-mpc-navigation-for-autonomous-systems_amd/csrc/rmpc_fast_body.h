@@ -540,6 +540,16 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
         } else if constexpr (PR == 2) gt.ld_pair(j, dst, pp);
         else gt.ld(j, dst);
     };
+    // Tile stores of unchanged gains skipped (config 3's instance, with GREG): a backward
+    // sweep forms block j's gains from the value function of the steps after j, so when the
+    // last set update changed nothing beyond step kmax, blocks j > kmax come out bitwise as the
+    // tile already holds them (the previous sweep stored them) and the lane does not store them
+    // again.  The first sweep of a launch stores every block.
+#ifndef RMPC_TILE_SKIP
+#define RMPC_TILE_SKIP 0
+#endif
+    constexpr bool TSKIP = RMPC_TILE_SKIP && GREG0 > 0 && PR == 1 && BS == 1 && UF;
+    int kmax = N;
     while (fin && it < maxit) {
         it++;
         // Keep the per-step inputs opaque to the optimiser at every iteration: otherwise it
@@ -715,7 +725,7 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
 #pragma unroll
                 for (int q = 0; q < 8; q++) asm volatile("" ::"v"(G[q]));
             } else if constexpr (PR == 2) gt.st_half(j, G, pp);
-            else gt.st(j, G);
+            else if (!TSKIP || j <= kmax) gt.st(j, G);
 #ifndef RMPC_BSB
 #define RMPC_BSB 0
 #endif
@@ -733,6 +743,7 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
         if constexpr (NO > 0) asm volatile("" ::: "memory");   // ... and the backward's row loads
         const T eps_h = SetTol<T>::hinge, eps_b = SetTol<T>::box;
         int changed = 0;
+        int kmax_n = -1;                   // (TSKIP) the last step whose sets this sweep changes
         used = 0;
         J = 0;
         T x0 = d0, x1 = d1, x2 = d2;
@@ -852,6 +863,7 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
                 }
                 Hf.set(k, hk ^ flips);
                 changed |= (int)chg;
+                if constexpr (TSKIP) kmax_n = chg ? k : kmax_n;
                 used |= (int)usd;
                 if constexpr (LTI) {
                     const T n0 = x0 + la0 * x2 + lb0 * u0v + S[k];
@@ -953,6 +965,7 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
             used |= (int)pair_xchg((uint32_t)used);
         }
         if (a.prof) tp_f += __builtin_amdgcn_s_memtime() - tp0;
+        if constexpr (TSKIP) kmax = kmax_n;
         if constexpr (RMPC_NOCERT) {
             asm volatile("" ::"v"(J), "v"(changed), "v"(used));
             continue;
