@@ -540,7 +540,7 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
         } else if constexpr (PR == 2) gt.ld_pair(j, dst, pp);
         else gt.ld(j, dst);
     };
-    // Tile stores of unchanged gains skipped (config 3's instance, with GREG): a backward
+    // Tile stores of unchanged gains skipped (LTV, block size 1, compile-time rows): a backward
     // sweep forms block j's gains from the value function of the steps after j, so when the
     // last set update changed nothing beyond step kmax, blocks j > kmax come out bitwise as the
     // tile already holds them (the previous sweep stored them) and the lane does not store them
@@ -548,7 +548,7 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
 #ifndef RMPC_TILE_SKIP
 #define RMPC_TILE_SKIP 0
 #endif
-    constexpr bool TSKIP = RMPC_TILE_SKIP && GREG0 > 0 && PR == 1 && BS == 1 && UF;
+    constexpr bool TSKIP = RMPC_TILE_SKIP && BS == 1 && UF && !LTI;
     int kmax = N;
     while (fin && it < maxit) {
         it++;
@@ -724,8 +724,9 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
             } else if constexpr (RMPC_GAIN_NOMEM && GREG > 0) {
 #pragma unroll
                 for (int q = 0; q < 8; q++) asm volatile("" ::"v"(G[q]));
-            } else if constexpr (PR == 2) gt.st_half(j, G, pp);
-            else if (!TSKIP || j <= kmax) gt.st(j, G);
+            } else if constexpr (PR == 2) {
+                if (!TSKIP || j <= kmax) gt.st_half(j, G, pp);
+            } else if (!TSKIP || j <= kmax) gt.st(j, G);
 #ifndef RMPC_BSB
 #define RMPC_BSB 0
 #endif
@@ -965,7 +966,10 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
             used |= (int)pair_xchg((uint32_t)used);
         }
         if (a.prof) tp_f += __builtin_amdgcn_s_memtime() - tp0;
-        if constexpr (TSKIP) kmax = kmax_n;
+        if constexpr (TSKIP) {             // (paired lanes: the pair's rows, both halves)
+            kmax = kmax_n;
+            if constexpr (PR == 2) kmax = max(kmax, (int)pair_xchg((uint32_t)kmax_n));
+        }
         if constexpr (RMPC_NOCERT) {
             asm volatile("" ::"v"(J), "v"(changed), "v"(used));
             continue;

@@ -11,4 +11,6 @@ tail -1 gpurun_out/tskip_suite.txt
 STEPS=50 timeout -k 10 400 bash scripts/ab.sh "--inflight 1" - "$K" - "$K" > gpurun_out/tskip_ab.txt 2>&1 || { cat gpurun_out/tskip_ab.txt; exit 1; }
 STEPS=100 timeout -k 10 600 bash scripts/ab.sh "" - "$K" - "$K" - "$K" >> gpurun_out/tskip_ab.txt 2>&1 || { cat gpurun_out/tskip_ab.txt; exit 1; }
 STEPS=20 timeout -k 10 600 bash scripts/ab.sh "" - "$K" - "$K" >> gpurun_out/tskip_ab.txt 2>&1 || { cat gpurun_out/tskip_ab.txt; exit 1; }
+STEPS=50 timeout -k 10 600 bash scripts/ab.sh "--config cfg4 --inflight 1" - "$K" - "$K" >> gpurun_out/tskip_ab.txt 2>&1 || { cat gpurun_out/tskip_ab.txt; exit 1; }
+STEPS=50 timeout -k 10 600 bash scripts/ab.sh "--config cfg4" - "$K" - "$K" >> gpurun_out/tskip_ab.txt 2>&1 || { cat gpurun_out/tskip_ab.txt; exit 1; }
 sed 's/RMPC_LIB_PATH=[^ ]*skip.so/skip/' gpurun_out/tskip_ab.txt | cut -c1-200
