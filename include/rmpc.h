@@ -28,8 +28,13 @@
  *     through device buffers it owns inside the context and returns after the results
  *     are back on the host (synchronous).  The _dev variants take DEVICE pointers and
  *     a hipStream_t (passed as void*; NULL = the null stream, as in HIP) and are
- *     asynchronous.  A context's scratch is shared by its _dev calls: issue them from one
- *     stream at a time per context.
+ *     asynchronous.  A context's scratch and its carried state (list counters, warm-start
+ *     sets, hybrid counters) are shared by its calls, which the library keeps in call order:
+ *     a call issued on another stream than the context's previous stateful call first makes
+ *     its stream wait for that call (an event recorded at the end of every stateful call), so
+ *     consecutive calls may use different streams.  Calls of one context must not be issued
+ *     concurrently from several host threads; batches meant to run at the same time use one
+ *     context each.  rmpc_ctx_destroy waits for the context's last call and side branch.
  *   - Return value: 0 on success, a negative RMPC_E* code on an API error (bad shape,
  *     null pointer, HIP failure).  rmpc_last_error() gives a thread-local message.
  *   - Numerical failure is never an API error: per robot, `status` says what happened

@@ -6,6 +6,7 @@
 // stream.  There is no CPU compute path: every result is produced by a HIP kernel.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -83,7 +84,6 @@ struct RmpcCtx {
     DevBuf pack;
     DevBuf idx_lqr, idx_mpc, counts, hyb_status;
     DevBuf fast_gains, retry, retry2, retry_count, prof, retry_sets;
-    DevBuf retry_a, retry_sets_a, retry_b, retry_sets_b;   // multi-pass fast stage: ping-pong lists and sets
     DevBuf refine, refine_sets;     // fp32 requests: the fp32-certified robots and their sets
     GroupDiag gdiag;           // lane-group tail diagnostics (RMPC_GROUP_CHECK, RMPC_DENSE_PROF=2)
     // closed-loop rollout state (rmpc_rollout_batch)
@@ -268,7 +268,11 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
         return RMPC_OK;
     }
     (void)hipSetDevice(c->device);
+    // every queued use of the buffers first: the context's stream, the last stateful call
+    // (which may have run on a caller stream, order_calls) and the side branch
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->last_valid && c->last_ev) (void)hipEventSynchronize(c->last_ev);
+    if (c->side) (void)hipStreamSynchronize(c->side);
     c->ws.release();
     for (auto &b : c->stage) b.release();
     c->pack.release();
@@ -295,10 +299,6 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     c->retry_sets_r.release();
     c->retry2.release();
     c->retry_sets.release();
-    c->retry_a.release();
-    c->retry_sets_a.release();
-    c->retry_b.release();
-    c->retry_sets_b.release();
     c->refine.release();
     c->refine_sets.release();
     c->warm_sets.release();
@@ -546,11 +546,7 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
     // re-certifies the fp32 pass's active sets: the soft LTV lane-per-robot instances with a
     // refinement pass (N = 20, and N = 30 with 8 obstacles).  Every other fp32 request runs the
     // fp64 pipeline, so every control an fp32 request returns is the fp64 optimum.
-    // (RMPC_NO_REFINE=1, diagnostics: fp32 arithmetic wherever an fp32 kernel exists, outputs
-    // fp32-rounded -- the round-2 behaviour)
-    const bool no_refine = rmpc_knob("RMPC_NO_REFINE") != nullptr;
-    const bool f32 = p->precision == RMPC_F32 &&
-                     (no_refine || (!lti && !hard && rmpc_mpc_refine_supported(p->horizon, bs, n_obs)));
+    const bool f32 = p->precision == RMPC_F32 && !lti && !hard && rmpc_mpc_refine_supported(p->horizon, bs, n_obs);
     const int prec = f32 ? RMPC_F32 : RMPC_F64;
     const bool fast = !hard && rmpc_mpc_fast_supported(p->horizon, bs, prec, lti, n_obs) &&
                       !rmpc_knob("RMPC_DISABLE_FAST");
@@ -572,11 +568,11 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
             list_n = cnt;
         }
         int32_t *cnt2 = cnt + 8;
-        const int cap = rmpc_knob("RMPC_LTI_CAP") ? atoi(rmpc_knob("RMPC_LTI_CAP")) : 11;
+        const int cap = 11;
         HIP_TRY(rmpc_launch_mpc_group(d, p->horizon, lti ? 1 : bs, n_obs, B, x0, x_refs, ref_rows, u_refs,
                                       uref_rows, obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
                                       iters, list, list_n, (int32_t *)c->retry2.p, cnt2, cap, nullptr, s, nullptr,
-                                      false, lti, &c->gdiag));
+                                      lti, &c->gdiag));
         dbg_sync(s, "group (cold)");
         HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
                                     step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
@@ -622,13 +618,9 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
                      : fast_cap > 0           ? fast_cap
                      : c->fast_cap > 0        ? c->fast_cap
                                               : (p->horizon <= 20 ? (lti ? 9 : 7) : 12);
-        const bool warm = !rmpc_knob("RMPC_COLD_TAIL");
-        a.init_zc = rmpc_knob("RMPC_INIT_ZC") ? atoi(rmpc_knob("RMPC_INIT_ZC")) : 0;
-
-        if (warm) {
-            HIP_TRY(c->retry_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
-            a.retry_sets = (uint32_t *)c->retry_sets.p;
-        }
+        // the tail continues from each handed-on robot's sets (retry_sets)
+        HIP_TRY(c->retry_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
+        a.retry_sets = (uint32_t *)c->retry_sets.p;
         // warm start across calls (rmpc_ctx_set_warm_start; warm_shift steps since the previous
         // call): the robots' previous certified sets, used by a robot whose last solve was the
         // previous call (stamps; the hybrid step's MPC branch takes a different subset each
@@ -672,33 +664,13 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
             HIP_TRY(hipMemsetAsync(pc, 0, 128 * sizeof(unsigned long long), s));
         }
         a.prof = pc;
-        // Multi-pass lane-per-robot stage (large batches, warm-started tail): pass i runs the
-        // robots the previous pass handed on for up to caps[i] PDAS solves in total, compacted
-        // into dense waves and continued from their sets (MpcFastArgs::warm_sets); the last pass
-        // runs up to the stage cap and hands on to the tail.  A robot's iterate path is the
-        // one-pass path (the cycle history resumes from the sets' signature); what changes is
-        // that a later pass's wave holds no robot that has already finished: at BASELINE
-        // config 3, 67% of the robots certify in their first solve, but a 64-robot wave almost
-        // always holds one that needs 3-7.  (RMPC_FAST_SPLIT=c1[,c2[,c3]]: the earlier passes'
-        // caps, A/B only; default one pass, HISTORY.md section 4)
-        int splits[3], nsplit = 0;
-        if (const char *sp = rmpc_knob("RMPC_FAST_SPLIT")) {
-            for (const char *q = sp; *q && nsplit < 3;) {
-                const int v = atoi(q);
-                if (v > (nsplit ? splits[nsplit - 1] : 0) && v < a.pdas_cap) splits[nsplit++] = v;
-                while (*q && *q != ',') q++;
-                if (*q == ',') q++;
-            }
-        }
-        if (!warm || B < 8192) nsplit = 0;
         // Mixed precision for fp32 requests (BASELINE config 4): the fp32 lane-per-robot pass
         // only finds the active sets.  Every robot it certifies goes on, with its sets, to an
         // fp64 pass of the same kernel that re-solves the equality-constrained QP of those sets
         // in fp64, re-checks them (KKT) and continues PDAS from them if they change (up to
         // `extra_cap` solves); it writes the outputs, which are therefore fp64-exact.  What it
-        // does not certify joins the fp64 tail's list.  (RMPC_NO_REFINE=1: the fp32 pass writes
-        // its own outputs, the round-2 behaviour; A/B only)
-        const bool refine = f32 && warm && rmpc_mpc_refine_supported(p->horizon, bs, n_obs) && !no_refine;
+        // does not certify joins the fp64 tail's list.
+        const bool refine = f32;
         if (refine) {
             HIP_TRY(c->refine.ensure((size_t)B * sizeof(int32_t)));
             HIP_TRY(c->refine_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
@@ -707,32 +679,13 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
             a.refine_sets = (uint32_t *)c->refine_sets.p;
         }
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[0], s));
-        {
-            DevBuf *lists[2] = {&c->retry_a, &c->retry_b}, *sets[2] = {&c->retry_sets_a, &c->retry_sets_b};
-            int32_t *pass_cnt[3] = {cnt + 2, cnt + 3, cnt + 5};
-            for (int i = 0; i < nsplit; i++) {
-                HIP_TRY(lists[i % 2]->ensure((size_t)B * sizeof(int32_t)));
-                HIP_TRY(sets[i % 2]->ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
-                MpcFastArgs ai = a;        // pass i: -> list i % 2 with its sets
-                ai.pdas_cap = splits[i];
-                ai.retry = (int32_t *)lists[i % 2]->p;
-                ai.retry_count = pass_cnt[i];
-                ai.retry_sets = (uint32_t *)sets[i % 2]->p;
-                HIP_TRY(rmpc_launch_mpc_fast(ai, p->horizon, bs, prec, s, lti));
-                dbg_sync(s, "fast pass");
-                a.index = ai.retry;        // the next pass: that list, from its sets
-                a.count = ai.retry_count;
-                a.warm_sets = ai.retry_sets;
-            }
-        }
         HIP_TRY(rmpc_launch_mpc_fast(a, p->horizon, bs, prec, s, lti));
         // tail: the lane-group Riccati kernel (RMPC_DISABLE_DENSE: no tail stage, A/B only)
         const bool group_tail = rmpc_mpc_group_supported(p->horizon, bs, n_obs) && !rmpc_knob("RMPC_DISABLE_DENSE");
         // The refinement and the tail work on disjoint robots (the fp32 pass's certified ones
         // and the rest): the refinement runs on the side stream while the tail runs here, and
         // the robots it hands on get a second, short tail launch after the join
-        // (RMPC_REFINE_INLINE=1: refinement, then one tail, on this stream; A/B)
-        const bool refine_side = refine && group_tail && c->use_side && !rmpc_knob("RMPC_REFINE_INLINE");
+        const bool refine_side = refine && group_tail && c->use_side;
         // Everything the side branch and the tails use is allocated before the fork, and every
         // error after the fork joins the side branch first (`join`): the call's stream must
         // never complete ahead of a refinement kernel that is still writing outputs.
@@ -771,7 +724,7 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
             // one fp64 solve from the fp32 sets: the robots whose sets it does not certify go
             // to the fp64 tail (config 4: 36.5M against 34.8M solves/s with 4 more solves here,
             // whose slowest waves set the pass's length)
-            r.extra_cap = rmpc_knob("RMPC_REFINE_CAP") ? atoi(rmpc_knob("RMPC_REFINE_CAP")) : 1;
+            r.extra_cap = 1;
             r.prof = pc ? pc + 64 : nullptr;   // (diagnostics: the refinement pass's own counters)
             hipStream_t rs = s;
             if (refine_side) {
@@ -790,64 +743,24 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
         const int32_t *left = (const int32_t *)c->retry.p;
         const int32_t *left_n = cnt;
         // tail PDAS cap before projected Newton (sweeps: 4 at N <= 20, 6 beyond -- config 4)
-        const int tail_cap = rmpc_knob("RMPC_DENSE_CAP") ? atoi(rmpc_knob("RMPC_DENSE_CAP"))
-                             : c->tail_cap > 0          ? c->tail_cap
-                                                        : (p->horizon <= 20 ? 4 : 6);
-        // a refined fp32 request always takes the fp64 tail (it returns fp64 optima only); the
-        // fp32 lane-group tail is a diagnostics variant (RMPC_TAIL32=1 with RMPC_NO_REFINE=1)
-        const bool tail32 = f32 && !refine && !rmpc_knob("RMPC_TAIL64") &&
-                            rmpc_mpc_group_supported(p->horizon, bs, n_obs, true);
+        const int tail_cap = c->tail_cap > 0 ? c->tail_cap : (p->horizon <= 20 ? 4 : 6);
+        // (a refined fp32 request takes the fp64 tail: it returns fp64 optima only)
         if (group_tail) {
             int32_t *cnt2 = cnt + 8;
             HIP_TRY_J(rmpc_launch_mpc_group(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs, uref_rows,
                                             obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
                                             iters, left, left_n, (int32_t *)c->retry2.p, cnt2, tail_cap,
-                                            a.retry_sets, s, pc, tail32, lti, &c->gdiag, a.prev_sets, a.prev_stamp));
+                                            a.retry_sets, s, pc, lti, &c->gdiag, a.prev_sets, a.prev_stamp));
             HIP_TRY(join());               // the refinement, before anything else on this stream
 #undef HIP_TRY_J
             if (refine_side) {            // the refinement's hand-ons (same output list)
                 HIP_TRY(rmpc_launch_mpc_group(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs, uref_rows,
                                               obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
                                               iters, (const int32_t *)c->retry_r.p, cnt + 10, (int32_t *)c->retry2.p,
-                                              cnt2, tail_cap, (const uint32_t *)c->retry_sets_r.p, s, pc, tail32, lti,
+                                              cnt2, tail_cap, (const uint32_t *)c->retry_sets_r.p, s, pc, lti,
                                               &c->gdiag, a.prev_sets, a.prev_stamp));
             }
-            if (prof) {
-                unsigned long long h[64];
-                int32_t cn[16];
-                HIP_TRY(hipMemcpyAsync(h, pc, sizeof(h), hipMemcpyDeviceToHost, s));
-                HIP_TRY(hipMemcpyAsync(cn, cnt, sizeof(cn), hipMemcpyDeviceToHost, s));
-                HIP_TRY(hipStreamSynchronize(s));
-                const double r = h[10] ? (double)h[10] : 1.0, li = h[9] ? (double)h[9] : 1.0;
-                fprintf(stderr,
-                        "[group] in=%d (+%d from the refinement) out=%d rounds=%llu loop-its/round %.2f | cycles/round: setup %.0f pn-pre %.0f "
-                        "out %.0f upd %.0f ls %.0f | per loop-it: weights %.0f back %.0f fwd %.0f rows %.0f\n",
-                        cn[0], cn[10], cn[8], h[10], h[9] / r, h[0] / r, h[1] / r, h[6] / r, h[7] / r, h[8] / r,
-                        h[2] / li, h[3] / li, h[4] / li, h[5] / li);
-                fprintf(stderr, "[group] tail iterations per robot:");
-                for (int q = 0; q < 32; q++) fprintf(stderr, " %llu", h[24 + q]);
-                fprintf(stderr, "\n");
-                const double w = h[20] ? (double)h[20] : 1.0;
-                fprintf(stderr, "[fast] waves=%llu per wave: total %.0f back %.0f fwd %.0f iters %.2f | per iter: back %.0f fwd %.0f"
-                        " | slowest wave: total %llu iters %llu back %llu%%\n",
-                        h[20], h[19] / w, h[16] / w, h[17] / w, h[18] / w, h[16] / (double)(h[18] ? h[18] : 1),
-                        h[17] / (double)(h[18] ? h[18] : 1), h[21] >> 16, (h[21] >> 8) & 0xff, h[21] & 0xff);
-                fprintf(stderr, "[fast] waves by loop count 0..7+:");
-                for (int q = 56; q < 64; q++) fprintf(stderr, " %llu", h[q]);
-                fprintf(stderr, " | setup %.0f per wave, longest lane entry-to-exit %llu, output pass %.0f per lane\n",
-                        h[22] / w, h[23], h[11] / (double)(h[12] ? h[12] : 1));
-                if (refine) {
-                    unsigned long long g[64];
-                    HIP_TRY(hipMemcpy(g, pc + 64, sizeof(g), hipMemcpyDeviceToHost));
-                    const double w2 = g[20] ? (double)g[20] : 1.0, i2 = g[18] ? (double)g[18] : 1.0;
-                    fprintf(stderr, "[refine] waves=%llu per wave: total %.0f back %.0f fwd %.0f iters %.2f setup %.0f | "
-                            "per iter: back %.0f fwd %.0f | slowest wave: total %llu iters %llu | loop counts 0..7+:",
-                            g[20], g[19] / w2, g[16] / w2, g[17] / w2, g[18] / w2, g[22] / w2, g[16] / i2, g[17] / i2,
-                            g[21] >> 16, (g[21] >> 8) & 0xff);
-                    for (int q = 56; q < 64; q++) fprintf(stderr, " %llu", g[q]);
-                    fprintf(stderr, "\n");
-                }
-            }
+            if (prof) HIP_TRY(rmpc_diag_print_stage_prof(pc, cnt, refine, s));
             dbg_sync(s, "group");
             left = (const int32_t *)c->retry2.p;
             left_n = cnt2;
@@ -856,12 +769,7 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
         // what remains is rare (cycling beyond both, non-finite data): LDS generic kernel, in
         // the requested arithmetic (the lane-group tail between is fp64 for both)
         // (a refined fp32 request stays fp64 here too: every output it returns is the fp64 optimum)
-        if (f32 && !refine)
-            HIP_TRY(rmpc_launch_mpc_f32(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
-                                        step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
-                                        c->ws.p, left, left_n, s, rmpc_mpc_lds_lanes(L), other_counts(c)));
-        else
-            HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
+        HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
                                         step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
                                         c->ws.p, left, left_n, s, rmpc_mpc_lds_lanes(L), other_counts(c)));
         if (B > 0) flip_counts(c);         // (the next pipeline takes the set zeroed there)
@@ -993,16 +901,24 @@ extern "C" int rmpc_mpc_solve_batch(RmpcCtx *c, const RmpcMpcParams *p, int64_t 
             memcpy(h + o_ur, u_refs, (size_t)B * uref_rows * 16);
             if (n_obs > 0) memcpy(h + o_ob, obstacles, (size_t)n_obs * 24);
             if (step_count) memcpy(h + o_sc, step_count, (size_t)B * 4);
-            HIP_TRY(hipMemcpyAsync(d, h, o_u0, hipMemcpyHostToDevice, own(c)));
             auto dp = [&](const void *user, size_t o) { return user ? (void *)(d + o) : nullptr; };
-            RC(rmpc_mpc_solve_batch_dev(c, p, B, (const double *)(d + o_x0), (const double *)(d + o_xr), ref_rows,
-                                        (const double *)(d + o_ur), uref_rows, n_obs > 0 ? (const double *)(d + o_ob) : nullptr,
-                                        n_obs, (int32_t *)dp(step_count, o_sc), (double *)(d + o_u0),
-                                        (double *)dp(u_seq, o_us), (double *)dp(x_pred, o_xp), (double *)dp(cost, o_co),
-                                        (int32_t *)(d + o_st), (uint8_t *)dp(slack_used, o_sl), (int32_t *)dp(iters, o_it),
-                                        own(c)));
-            HIP_TRY(hipMemcpyAsync(h + o_sc, d + o_sc, off - o_sc, hipMemcpyDeviceToHost, own(c)));
-            HIP_TRY(hipStreamSynchronize(own(c)));
+            // once the first copy is queued, every exit waits for the stream: a copy still
+            // reading the pinned block must not meet the next call's writes (or its regrowth)
+            const int rc = [&]() -> int {
+                HIP_TRY(hipMemcpyAsync(d, h, o_u0, hipMemcpyHostToDevice, own(c)));
+                RC(rmpc_mpc_solve_batch_dev(c, p, B, (const double *)(d + o_x0), (const double *)(d + o_xr), ref_rows,
+                                            (const double *)(d + o_ur), uref_rows,
+                                            n_obs > 0 ? (const double *)(d + o_ob) : nullptr, n_obs,
+                                            (int32_t *)dp(step_count, o_sc), (double *)(d + o_u0),
+                                            (double *)dp(u_seq, o_us), (double *)dp(x_pred, o_xp),
+                                            (double *)dp(cost, o_co), (int32_t *)(d + o_st),
+                                            (uint8_t *)dp(slack_used, o_sl), (int32_t *)dp(iters, o_it), own(c)));
+                HIP_TRY(hipMemcpyAsync(h + o_sc, d + o_sc, off - o_sc, hipMemcpyDeviceToHost, own(c)));
+                return RMPC_OK;
+            }();
+            const hipError_t es = hipStreamSynchronize(own(c));
+            if (rc != RMPC_OK) return rc;
+            HIP_TRY(es);
             if (step_count) memcpy(step_count, h + o_sc, (size_t)B * 4);
             memcpy(u0, h + o_u0, (size_t)B * 16);
             if (u_seq) memcpy(u_seq, h + o_us, (size_t)B * N * 16);
@@ -1544,3 +1460,48 @@ extern "C" int rmpc_rollout_batch(RmpcCtx *c, const RmpcRolloutParams *rp, const
     HIP_TRY(hipStreamSynchronize(own(c)));
     return RMPC_OK;
 }
+
+#if RMPC_WAVE_LOG
+// ---- wave timeline log (diagnostics builds only, rmpc_wlog.h): begin allocates `cap` records
+// on the current device and arms the MPC kernels' logs; end synchronises the device, copies the
+// records shard by shard, packed, into `host` ([cap][4] uint64) and returns their number
+// (-2 - n if a shard overflowed).
+extern "C" hipError_t rmpc_wlog_set_fast(rmpc::WaveLog);
+extern "C" hipError_t rmpc_wlog_set_group(rmpc::WaveLog);
+extern "C" hipError_t rmpc_wlog_set_solve(rmpc::WaveLog);
+static rmpc::WaveLog g_host_wlog = {nullptr, nullptr, 0};
+extern "C" int rmpc_diag_wlog_begin(uint32_t cap) {
+    if (!g_host_wlog.rec) {
+        if (hipMalloc((void **)&g_host_wlog.rec, (size_t)cap * 32) != hipSuccess) return -1;
+        if (hipMalloc((void **)&g_host_wlog.n, 64 * 128) != hipSuccess) return -1;
+        g_host_wlog.cap = cap;
+    }
+    if (hipDeviceSynchronize() != hipSuccess || hipMemset(g_host_wlog.n, 0, 64 * 128) != hipSuccess) return -1;
+    if (rmpc_wlog_set_fast(g_host_wlog) != hipSuccess || rmpc_wlog_set_group(g_host_wlog) != hipSuccess ||
+        rmpc_wlog_set_solve(g_host_wlog) != hipSuccess)
+        return -1;
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+extern "C" int64_t rmpc_diag_wlog_end(void *host, uint32_t cap) {
+    if (!g_host_wlog.rec || hipDeviceSynchronize() != hipSuccess) return -1;
+    const rmpc::WaveLog off = {nullptr, nullptr, 0};
+    unsigned n[64 * 32];
+    if (hipMemcpy(n, g_host_wlog.n, sizeof n, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    const unsigned per = g_host_wlog.cap / 64u;
+    int64_t m = 0;
+    bool over = false;
+    for (int s = 0; s < 64; s++) {
+        unsigned k = n[32 * s];
+        if (k > per) { over = true; k = per; }
+        if (m + k > cap) { over = true; k = (unsigned)(cap - m); }
+        if (k && hipMemcpy((char *)host + m * 32, g_host_wlog.rec + 4ull * per * s, (size_t)k * 32,
+                           hipMemcpyDeviceToHost) != hipSuccess)
+            return -1;
+        m += k;
+    }
+    if (rmpc_wlog_set_fast(off) != hipSuccess || rmpc_wlog_set_group(off) != hipSuccess ||
+        rmpc_wlog_set_solve(off) != hipSuccess)
+        return -1;
+    return over ? -2 - m : m;
+}
+#endif

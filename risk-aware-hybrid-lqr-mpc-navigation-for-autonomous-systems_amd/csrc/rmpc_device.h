@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "../../include/rmpc.h"
+#include "rmpc_wlog.h"
 
 #define RMPC_PI 3.141592653589793
 #define RMPC_WAVE 64

@@ -451,46 +451,6 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
             Bf.set(j, v);
         }
     }
-#ifndef RMPC_INIT_ZC_BUILD
-#define RMPC_INIT_ZC_BUILD 1
-#endif
-    else if (RMPC_INIT_ZC_BUILD && a.init_zc) {
-        // Zero-correction start: the hinge rows the reference inputs alone would violate start
-        // active (the free response x_{k+1} = A_k x_k (+ c_k), du = 0).  The QP and its optimum
-        // are unchanged; only the first PDAS iterate is closer to it.
-        T x0 = d0, x1 = d1, x2 = d2;
-#pragma unroll
-        for (int k = 0; k < N; k++) {
-            if (k > 0) {
-                const T px = PX(k), py = PY(k);
-                uint32_t h = 0;
-#pragma unroll
-                for (int o = 0; o < (NO > 0 ? NOL : RMPC_MAX_OBSTACLES); o++) {
-                    if (NO == 0 && o >= a.no) break;
-                    const T ox = obs_s[3 * (obase + o)], oy = obs_s[3 * (obase + o) + 1], sf = obs_s[3 * (obase + o) + 2];
-                    const T ddx = px - ox, ddy = py - oy;
-                    const T dd = ddx * ddx + ddy * ddy;
-                    T y = rsq_approx(dd);
-                    if constexpr (F64) {
-                        const T hh = (T)0.5 * dd * y;
-                        y = fma(y, fma(-hh, y, (T)0.5), y);
-                    }
-                    const T r = fma(-fma(ddy, x1, fma(ddx, x0, dd)), y, sf);
-                    h |= (dd * y > (T)0.01 && r > (T)0) ? (1u << o) : 0u;
-                }
-                Hf.set(k, h);
-            }
-            if constexpr (LTI) {
-                const T n0 = x0 + la0 * x2 + S[k], n1 = x1 + la1 * x2 + Cs[k];
-                x2 = x2 + V0[k];
-                x0 = n0; x1 = n1;
-            } else {
-                const T vr = fabs(V0[k]) > (T)0.01 ? V0[k] : (T)0.1;
-                x0 = x0 + (-vr * S[k] * dt) * x2;
-                x1 = x1 + (vr * Cs[k] * dt) * x2;
-            }
-        }
-    }
     // (fp64 refinement of fp32-certified sets: `extra_cap` more PDAS solves from them)
     const int maxit = a.extra_cap > 0 ? min(p.max_iter, it + a.extra_cap) : maxit0;
     // The last GREG blocks the backward sweep forms (j < GREG) stay in registers instead of the
@@ -540,16 +500,6 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
         } else if constexpr (PR == 2) gt.ld_pair(j, dst, pp);
         else gt.ld(j, dst);
     };
-    // Tile stores of unchanged gains skipped (LTV, block size 1, compile-time rows): a backward
-    // sweep forms block j's gains from the value function of the steps after j, so when the
-    // last set update changed nothing beyond step kmax, blocks j > kmax come out bitwise as the
-    // tile already holds them (the previous sweep stored them) and the lane does not store them
-    // again.  The first sweep of a launch stores every block.
-#ifndef RMPC_TILE_SKIP
-#define RMPC_TILE_SKIP 0
-#endif
-    constexpr bool TSKIP = RMPC_TILE_SKIP && BS == 1 && UF && !LTI;
-    int kmax = N;
     while (fin && it < maxit) {
         it++;
         // Keep the per-step inputs opaque to the optimiser at every iteration: otherwise it
@@ -725,8 +675,8 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
 #pragma unroll
                 for (int q = 0; q < 8; q++) asm volatile("" ::"v"(G[q]));
             } else if constexpr (PR == 2) {
-                if (!TSKIP || j <= kmax) gt.st_half(j, G, pp);
-            } else if (!TSKIP || j <= kmax) gt.st(j, G);
+                gt.st_half(j, G, pp);
+            } else gt.st(j, G);
 #ifndef RMPC_BSB
 #define RMPC_BSB 0
 #endif
@@ -744,7 +694,6 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
         if constexpr (NO > 0) asm volatile("" ::: "memory");   // ... and the backward's row loads
         const T eps_h = SetTol<T>::hinge, eps_b = SetTol<T>::box;
         int changed = 0;
-        int kmax_n = -1;                   // (TSKIP) the last step whose sets this sweep changes
         used = 0;
         J = 0;
         T x0 = d0, x1 = d1, x2 = d2;
@@ -864,7 +813,6 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
                 }
                 Hf.set(k, hk ^ flips);
                 changed |= (int)chg;
-                if constexpr (TSKIP) kmax_n = chg ? k : kmax_n;
                 used |= (int)usd;
                 if constexpr (LTI) {
                     const T n0 = x0 + la0 * x2 + lb0 * u0v + S[k];
@@ -966,10 +914,6 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
             used |= (int)pair_xchg((uint32_t)used);
         }
         if (a.prof) tp_f += __builtin_amdgcn_s_memtime() - tp0;
-        if constexpr (TSKIP) {             // (paired lanes: the pair's rows, both halves)
-            kmax = kmax_n;
-            if constexpr (PR == 2) kmax = max(kmax, (int)pair_xchg((uint32_t)kmax_n));
-        }
         if constexpr (RMPC_NOCERT) {
             asm volatile("" ::"v"(J), "v"(changed), "v"(used));
             continue;

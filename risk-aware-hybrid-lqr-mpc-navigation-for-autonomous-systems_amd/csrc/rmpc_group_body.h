@@ -40,7 +40,6 @@ struct GroupArgs {
     int32_t *retry, *retry_count;     // not certified / non-finite -> generic kernel
     const uint32_t *warm;             // per list entry: hinge flags [N], box states [NB], iters
     int pdas_cap;                     // PDAS solves before projected Newton
-    double ls_beta;                   // Armijo backtracking: > 0 fixed factor, 0 quadratic interpolation
     unsigned long long *prof;         // optional per-phase cycle counters (diagnostics)
     unsigned long long *prof_waves;   // optional per-wave phase records (RMPC_DENSE_PROF=2)
     int64_t nB;                       // rows of the per-robot output arrays (bounds checks)
@@ -1389,9 +1388,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
                         F = Ft;
                         searching = false;
                     }
-                    if (a.ls_beta > 0) {
-                        alpha *= (T)a.ls_beta;
-                    } else {       // safeguarded quadratic interpolation: q(s) = F + gd s + c s^2, q(1) = Ft
+                    {              // safeguarded quadratic interpolation: q(s) = F + gd s + c s^2, q(1) = Ft
                         const T c = Ft - F - gd;
                         const T s = c > (T)0 ? -gd / ((T)2 * c) : (T)0.5;
                         alpha *= fmin(fmax(s, (T)0.1), (T)0.5);
@@ -1418,7 +1415,7 @@ __device__ __forceinline__ void group_solve(const GroupArgs &a, T *const base0,
                     F = Ft;
                     searching = false;
                 }
-                alpha *= (T)(a.ls_beta > 0 ? a.ls_beta : 0.5);   // (block size > 1: fixed factor)
+                alpha *= (T)0.5;                 // (block size > 1: fixed factor)
                 __syncthreads();
             }
             if (searching) fail = true;          // no acceptable step

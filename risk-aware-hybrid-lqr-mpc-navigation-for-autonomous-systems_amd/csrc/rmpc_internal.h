@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "../../include/rmpc.h"
+#include "rmpc_wlog.h"
 
 #define RMPC_PDAS_ITERS 32   // PDAS solves before the projected-Newton phase
 
@@ -75,7 +76,6 @@ struct MpcFastArgs {
     // outputs; uncertified ones still go to `retry`
     int32_t *refine, *refine_count;
     uint32_t *refine_sets;
-    int init_zc;                     // cold start: hinge rows violated by the free response start active
     // Warm start across calls (rmpc_ctx_set_warm_start): per ROBOT b, the active sets of its
     // previous certified solve, slot-minor [N + NB + 1][B] (hinge flags, box states, the stamp
     // of the call that wrote them); read shifted by prev_shift steps at the start (the last step
@@ -108,7 +108,9 @@ struct GroupDiag {
     void release();
 };
 
-bool rmpc_mpc_group_supported(int N, int bs, int no, bool f32 = false);
+bool rmpc_mpc_group_supported(int N, int bs, int no);
+// diagnostics output (rmpc_diag.cpp; RMPC_DIAG=1 with RMPC_DENSE_PROF=1)
+hipError_t rmpc_diag_print_stage_prof(const unsigned long long *pc, const int32_t *cnt, bool refine, hipStream_t s);
 hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no, int64_t capacity,
                                  const double *x0, const double *x_refs, int ref_rows,
                                  const double *u_refs, int uref_rows, const double *obstacles,
@@ -116,7 +118,7 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
                                  double *cost, int32_t *status, uint8_t *slack_used, int32_t *iters,
                                  const int32_t *index, const int32_t *count, int32_t *retry,
                                  int32_t *retry_count, int pdas_cap, const uint32_t *warm,
-                                 hipStream_t stream, unsigned long long *prof = nullptr, bool f32 = false,
+                                 hipStream_t stream, unsigned long long *prof = nullptr,
                                  bool lti = false, GroupDiag *diag = nullptr, uint32_t *prev_sets = nullptr,
                                  uint32_t prev_stamp = 0);
 

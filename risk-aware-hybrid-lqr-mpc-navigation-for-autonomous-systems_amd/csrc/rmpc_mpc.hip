@@ -625,6 +625,7 @@ __device__ __forceinline__ void mpc_solve_one(const MpcArgs<T> &a, int64_t t) {
 // workgroups that each hold 128 KB of LDS only to exit
 template <typename T, bool USE_LDS>
 __global__ __launch_bounds__(256) void mpc_solve_kernel(MpcArgs<T> a) {
+    RMPC_WLOG_BEGIN
     const int64_t nrob = a.index ? (int64_t)*a.count : a.B;
     const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (a.zero_next && t0 == 0)
@@ -634,12 +635,14 @@ __global__ __launch_bounds__(256) void mpc_solve_kernel(MpcArgs<T> a) {
     } else {
         if (t0 < nrob) mpc_solve_one<T, false>(a, t0);
     }
+    RMPC_WLOG_END(WL_SOLVE)
 }
 
 }  // namespace rmpc
 
 // ------------------------------------------------------------------------------ launcher
 using namespace rmpc;
+RMPC_WLOG_SETTER(rmpc_wlog_set_solve)
 
 MpcLayout rmpc_mpc_layout(int N, int bs, int no) {
     MpcLayout L;

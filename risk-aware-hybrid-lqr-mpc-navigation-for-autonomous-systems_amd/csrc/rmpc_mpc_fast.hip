@@ -23,19 +23,21 @@
 namespace rmpc {
 template <int N, int BS, typename T, bool LTI, int NO = 0, int PR = 1, bool WS = true>
 __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
+    RMPC_WLOG_BEGIN
     fast_body<N, BS, T, LTI, NO, PR, WS>(a, blockIdx.x);
+    RMPC_WLOG_END(WL_FAST)
 }
 }  // namespace rmpc
+RMPC_WLOG_SETTER(rmpc_wlog_set_fast)
 
 using namespace rmpc;
 
 
 bool rmpc_mpc_fast_supported(int N, int bs, int prec, bool lti, int no) {
     if (lti) return prec != RMPC_F32 && (N == 6 || N == 10 || N == 20);   // LTI: block size unused
-    if (prec == RMPC_F32) return bs == 1 && (N == 20 || N == 30);
+    if (prec == RMPC_F32) return bs == 1 && (N == 20 || (N == 30 && no == 8));   // the refined shapes
     // fp64 N = 30: the paired-lane 8-obstacle instance (BASELINE config 4's shape) only
-    // (RMPC_NO_F64_N30=1: the lane-group path from a cold start, the round-2 route; A/B)
-    if (bs == 1 && N == 30) return no == 8 && !rmpc_knob("RMPC_NO_F64_N30");
+    if (bs == 1 && N == 30) return no == 8;
     return (bs == 1 && (N == 6 || N == 10 || N == 20)) || (bs == 2 && N == 6);
 }
 
@@ -54,24 +56,17 @@ hipError_t rmpc_launch_mpc_fast(const MpcFastArgs &a, int N, int bs, int prec, h
                        (size_t)RMPC_WAVE * 17 * sizeof(double);
     const size_t lds2 = (size_t)3 * N * (RMPC_WAVE / 2) * (prec == RMPC_F32 ? sizeof(float) : sizeof(double)) +
                         (size_t)(RMPC_WAVE / 2) * 17 * sizeof(double);
-    // RMPC_FAST_NOSPEC=1: runtime obstacle loop even where a compile-time instance exists (A/B)
-    const char *ns_e = rmpc_knob("RMPC_FAST_NOSPEC");
-    const bool nospec = ns_e && *ns_e == '1';
     if (lti) {
         if (prec == RMPC_F32) return hipErrorInvalidValue;
-        if (N == 20 && a.no == 3 && !nospec) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, true, 3>), grid, block, lds, stream, a);
+        if (N == 20 && a.no == 3) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, true, 3>), grid, block, lds, stream, a);
         else if (N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, true>), grid, block, lds, stream, a);
         else if (N == 10) hipLaunchKernelGGL((mpc_ltv_fast_kernel<10, 1, double, true>), grid, block, lds, stream, a);
         else if (N == 6) hipLaunchKernelGGL((mpc_ltv_fast_kernel<6, 1, double, true>), grid, block, lds, stream, a);
         else return hipErrorInvalidValue;
     } else if (prec == RMPC_F32) {
-        // paired lanes for the 8-obstacle N = 30 instance (RMPC_FAST_PAIR=0: one lane per robot, A/B)
-        const char *pr_e = rmpc_knob("RMPC_FAST_PAIR");
-        const bool pair = !(pr_e && *pr_e == '0');
+        // paired lanes for the 8-obstacle N = 30 instance
         const dim3 grid2((unsigned)((n + RMPC_WAVE / 2 - 1) / (RMPC_WAVE / 2)));
-        if (bs == 1 && N == 30 && a.no == 8 && !nospec && pair) hipLaunchKernelGGL((mpc_ltv_fast_kernel<30, 1, float, false, 8, 2>), grid2, block, lds2, stream, a);
-        else if (bs == 1 && N == 30 && a.no == 8 && !nospec) hipLaunchKernelGGL((mpc_ltv_fast_kernel<30, 1, float, false, 8>), grid, block, lds, stream, a);
-        else if (bs == 1 && N == 30) hipLaunchKernelGGL((mpc_ltv_fast_kernel<30, 1, float, false>), grid, block, lds, stream, a);
+        if (bs == 1 && N == 30 && a.no == 8) hipLaunchKernelGGL((mpc_ltv_fast_kernel<30, 1, float, false, 8, 2>), grid2, block, lds2, stream, a);
         else if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, float, false>), grid, block, lds, stream, a);
         else return hipErrorInvalidValue;
     } else {
@@ -79,8 +74,8 @@ hipError_t rmpc_launch_mpc_fast(const MpcFastArgs &a, int N, int bs, int prec, h
         // (N = 30, 8 obstacles in fp64: paired lanes -- fp64 requests and the fp32 requests'
         // refinement pass)
         if (bs == 1 && N == 30 && a.no == 8) hipLaunchKernelGGL((mpc_ltv_fast_kernel<30, 1, double, false, 8, 2>), grid2, block, lds2, stream, a);
-        else if (bs == 1 && N == 20 && a.no == 3 && !nospec && a.prev_sets) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, false, 3>), grid, block, lds, stream, a);
-        else if (bs == 1 && N == 20 && a.no == 3 && !nospec) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, false, 3, 1, false>), grid, block, lds, stream, a);
+        else if (bs == 1 && N == 20 && a.no == 3 && a.prev_sets) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, false, 3>), grid, block, lds, stream, a);
+        else if (bs == 1 && N == 20 && a.no == 3) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, false, 3, 1, false>), grid, block, lds, stream, a);
         else if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, false>), grid, block, lds, stream, a);
         else if (bs == 1 && N == 10) hipLaunchKernelGGL((mpc_ltv_fast_kernel<10, 1, double, false>), grid, block, lds, stream, a);
         else if (bs == 1 && N == 6) hipLaunchKernelGGL((mpc_ltv_fast_kernel<6, 1, double, false>), grid, block, lds, stream, a);

@@ -30,42 +30,42 @@
 
 namespace rmpc {
 
-// One wave per workgroup, 64/G list entries per wave, one round: the grid covers the list's
-// capacity and waves past the device-side count exit at once (measured free next to the
-// tail's run time).  A persistent variant that looped over rounds faulted from its second
-// round on (every robot's accesses in bounds, checked with RMPC_GROUP_CHECK), so there is
-// no round loop.
-//
-// PERSIST (diagnostics only, RMPC_GROUP_PERSIST=<waves per CU>): the former persistent form,
-// a capped grid looping over rounds, kept to reproduce the round-1 fault under the
-// RMPC_GROUP_CHECK instrumentation.
-template <int N, int BS, int G, typename T, bool LTI, bool PERSIST = false>
+// One wave per workgroup, 64/G list entries per wave per round.  The grid is capped
+// (rmpc_launch_mpc_group: GROUP_GRID_MAX waves, fewer when the list's capacity is smaller) and
+// the waves loop over rounds until the device-side count is covered; every wave reads the same
+// count, so every wave reaches the exit.  The list's capacity is the whole batch, but a launch
+// hands a few thousand robots to this stage: a grid over the capacity (16384 one-wave
+// workgroups at config 3, ~950 with work) kept the SIMDs it passed through idle for 28% of the
+// in-flight run, one dispatch gap per empty workgroup (profiles/r05/wave_timeline_*.json).
+// (Round 1's persistent form faulted beyond its first round; that tree's tail is gone, and
+// round 2 ran this loop with every config-3 robot through it, 16 rounds per wave, bounds-checked
+// and bitwise equal: HISTORY.md section 3.)
+template <int N, int BS, int G, typename T, bool LTI>
 __global__ __launch_bounds__(64, 1) void mpc_group_kernel(GroupArgs a) {
     constexpr int NB = (N + BS - 1) / BS, RPW = 64 / G;
+    RMPC_WLOG_BEGIN
     extern __shared__ double lds_raw[];
     T *const lds = reinterpret_cast<T *>(lds_raw);
     const int lane = threadIdx.x, gl = lane % G, grp = lane / G;
     const int rec = GRec<N, NB, T>::size(a.no);
     const int cnt = *a.count;
     if (a.chk && lane == 0 && blockIdx.x == 0 && (cnt < 0 || cnt > a.nB)) diag_hit(a.chk, 2, 4, cnt);
-    if constexpr (PERSIST) {
-        for (int t0 = blockIdx.x * RPW; t0 < cnt; t0 += gridDim.x * RPW) {
-            const int t = t0 + grp;
-            group_solve<N, BS, G, T, LTI>(a, lds + grp * rec, t, t < cnt, gl, grp);
-            __syncthreads();
-        }
-    } else {
-        const int t0 = blockIdx.x * RPW;
-        if (t0 >= cnt) return;
+    for (int t0 = blockIdx.x * RPW; t0 < cnt; t0 += gridDim.x * RPW) {
         const int t = t0 + grp;
         group_solve<N, BS, G, T, LTI>(a, lds + grp * rec, t, t < cnt, gl, grp);
+        __syncthreads();           // (the next round rewrites the groups' LDS records)
     }
     GSITE(8);
+    RMPC_WLOG_END(WL_GROUP)
 }
 
 }  // namespace rmpc
 
 using namespace rmpc;
+RMPC_WLOG_SETTER(rmpc_wlog_set_group)
+
+// the tail's grid cap in waves (1024: one per SIMD of the chip)
+#define GROUP_GRID_MAX 1024
 
 void GroupDiag::release() {
     if (pw) (void)hipFree(pw);
@@ -74,16 +74,13 @@ void GroupDiag::release() {
     pw = nullptr; pw_cap = 0; chk_host = nullptr; site_host = nullptr; site_cap = 0;
 }
 
-// fp32 instances (the LTV fp32 fast instances' shapes, N = 20 / 30): opt-in, RMPC_TAIL32=1.
-// Faster than the fp64 tail at config 4 (42.9M against 38.7M solves/s) since packed-fp32 code
-// is no longer generated (HISTORY.md section 4), but with every robot routed through it the
-// fp32 tail's control error reached 1.9e-4 relative, above the north star's 1e-4.
-bool rmpc_mpc_group_supported(int N, int bs, int no, bool f32) {
-    if (f32 && !(bs == 1 && (N == 20 || N == 30) && rmpc_knob("RMPC_TAIL32") && atoi(rmpc_knob("RMPC_TAIL32")) > 0))
-        return false;
+// fp64 only: a refined fp32 request's tail is fp64 too (it returns fp64 optima).  (An fp32 tail
+// ran config 4 faster, 42.9M against 38.7M solves/s, but with every robot routed through it its
+// control error reached 1.9e-4 relative, above the north star's 1e-4: removed, HISTORY.md.)
+bool rmpc_mpc_group_supported(int N, int bs, int no) {
     const bool inst = (bs == 1 && (N == 6 || N == 10 || N == 20 || N == 30)) || (bs == 2 && N == 6);
     if (!inst || no > 16) return false;
-    const size_t lds = (size_t)(64 / group_lanes(N, bs)) * group_rec_bytes(N, bs, no, f32);
+    const size_t lds = (size_t)(64 / group_lanes(N, bs)) * group_rec_bytes(N, bs, no, false);
     return lds <= 160 * 1024;
 }
 
@@ -94,10 +91,10 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
                                  double *cost, int32_t *status, uint8_t *slack_used, int32_t *iters,
                                  const int32_t *index, const int32_t *count, int32_t *retry,
                                  int32_t *retry_count, int pdas_cap, const uint32_t *warm,
-                                 hipStream_t stream, unsigned long long *prof, bool f32, bool lti,
+                                 hipStream_t stream, unsigned long long *prof, bool lti,
                                  GroupDiag *diag, uint32_t *prev_sets, uint32_t prev_stamp) {
     if (capacity <= 0) return hipSuccess;
-    if (!rmpc_mpc_group_supported(N, bs, no, f32) || (lti && bs != 1) || (f32 && lti)) return hipErrorInvalidValue;
+    if (!rmpc_mpc_group_supported(N, bs, no) || (lti && bs != 1)) return hipErrorInvalidValue;
     GroupArgs a;
     a.prm = prm;
     a.no = no;
@@ -117,9 +114,10 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
     a.prev_stamp = prev_stamp;
     const int G = group_lanes(N, bs), rpw = 64 / G;
     const int64_t need = (capacity + rpw - 1) / rpw;
-    // RMPC_GROUP_PERSIST=<waves per CU> (diagnostics): capped grid looping over rounds
-    const int persist = rmpc_knob("RMPC_GROUP_PERSIST") ? atoi(rmpc_knob("RMPC_GROUP_PERSIST")) : 0;
-    const int64_t grid = persist > 0 ? (need < 256 * persist ? need : 256 * persist) : need;
+    // capped grid (the kernel loops over rounds): GROUP_GRID_MAX waves, one per SIMD of the chip
+    // (RMPC_GROUP_GRID=<waves>: another cap, A/B)
+    const int64_t gmax = rmpc_knob("RMPC_GROUP_GRID") ? atoll(rmpc_knob("RMPC_GROUP_GRID")) : GROUP_GRID_MAX;
+    const int64_t grid = need < gmax ? need : (gmax > 0 ? gmax : need);
     // diagnostics buffers (RMPC_DENSE_PROF=2, RMPC_GROUP_CHECK): owned by the caller's context
     const char *pe = rmpc_knob("RMPC_DENSE_PROF");
     if (diag && prof && pe && atoi(pe) >= 2) {
@@ -163,26 +161,14 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
         }
     }
     a.pdas_cap = pdas_cap < RMPC_PDAS_ITERS ? pdas_cap : RMPC_PDAS_ITERS;
-    // Armijo backtracking: safeguarded quadratic interpolation (0, the default), or a fixed
-    // factor in (0, 1) (RMPC_LS_BETA, A/B only); anything outside (0, 1) means the default
-    const double beta = rmpc_knob("RMPC_LS_BETA") ? atof(rmpc_knob("RMPC_LS_BETA")) : 0.0;
-    a.ls_beta = (beta > 0.0 && beta < 1.0) ? beta : 0.0;
-    const size_t lds = (size_t)rpw * group_rec_bytes(N, bs, no, f32);
+    const size_t lds = (size_t)rpw * group_rec_bytes(N, bs, no, false);
     const dim3 g((unsigned)grid), blk(64);
 #define GK(n, b, g, t, l) (const void *)mpc_group_kernel<n, b, g, t, l>
-    const void *fn;
-    if (f32) {
-        fn = N == 30 ? GK(30, 1, 32, float, false) : GK(20, 1, 16, float, false);
-    } else if (persist > 0) {
-        if (!(bs == 1 && N == 20 && !lti)) return hipErrorInvalidValue;   // the round-1 fault's shape
-        fn = (const void *)mpc_group_kernel<20, 1, 16, double, false, true>;
-    } else {
-        fn = (bs == 1 && N == 30)   ? (lti ? GK(30, 1, 32, double, true) : GK(30, 1, 32, double, false))
-             : (bs == 1 && N == 20) ? (lti ? GK(20, 1, 16, double, true) : GK(20, 1, 16, double, false))
-             : (bs == 1 && N == 10) ? (lti ? GK(10, 1, 16, double, true) : GK(10, 1, 16, double, false))
-             : (bs == 1 && N == 6)  ? (lti ? GK(6, 1, 16, double, true) : GK(6, 1, 16, double, false))
-                                    : GK(6, 2, 16, double, false);
-    }
+    const void *fn = (bs == 1 && N == 30)   ? (lti ? GK(30, 1, 32, double, true) : GK(30, 1, 32, double, false))
+                     : (bs == 1 && N == 20) ? (lti ? GK(20, 1, 16, double, true) : GK(20, 1, 16, double, false))
+                     : (bs == 1 && N == 10) ? (lti ? GK(10, 1, 16, double, true) : GK(10, 1, 16, double, false))
+                     : (bs == 1 && N == 6)  ? (lti ? GK(6, 1, 16, double, true) : GK(6, 1, 16, double, false))
+                                            : GK(6, 2, 16, double, false);
 #undef GK
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -216,9 +202,9 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
     if (a.chk) {                  // read from host-mapped memory: valid even if the launch faulted
         const hipError_t e = hipStreamSynchronize(stream);
         const int32_t *r = diag->chk_host;
-        fprintf(stderr, "[group check] %s grid %lld persist %d: flags %d (1 robot index, 2 list count, 4 retry slot, "
-                "8 list entry) first site %d value %d block %d; launch: %s\n", f32 ? "fp32" : "fp64", (long long)grid,
-                persist, r[0], r[1], r[2], r[3], hipGetErrorString(e));
+        fprintf(stderr, "[group check] grid %lld: flags %d (1 robot index, 2 list count, 4 retry slot, "
+                "8 list entry) first site %d value %d block %d; launch: %s\n", (long long)grid,
+                r[0], r[1], r[2], r[3], hipGetErrorString(e));
         if (a.site) {             // waves by last site reached (8 = exited)
             long long hist[16] = {0};
             for (int64_t w = 0; w < grid; w++) hist[diag->site_host[w] & 15]++;

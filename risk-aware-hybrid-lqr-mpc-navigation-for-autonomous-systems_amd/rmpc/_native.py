@@ -6,6 +6,7 @@ entry point raises.  The library is built in-tree by ``__graft_entry__.build()``
 """
 import ctypes as C
 import os
+import weakref
 import threading
 
 import numpy as np
@@ -205,6 +206,20 @@ def own_context(device=0):
 def release_context(h):
     if h is not None and _lib is not None:
         _lib.rmpc_ctx_destroy(h)
+
+
+class OwnedContext:
+    """One caller's own context (own_context), destroyed exactly once: by release(), or by a
+    weakref finalizer when the owner is collected (also at interpreter exit, before the
+    library's own teardown).  Copies of the owning object must not share it (MPCController
+    resets its owner on copy)."""
+
+    def __init__(self, device=0):
+        self.h = own_context(device)
+        self._fin = weakref.finalize(self, release_context, self.h)
+
+    def release(self):
+        self._fin()
 
 
 def ptr(a):

@@ -96,7 +96,7 @@ class MPCController:
         # previous certified active sets (rmpc_ctx_set_warm_start), shifted by one step.  Same
         # optimum, fewer PDAS iterations.  warm_start=False: the shared context, cold solves.
         self.warm_start = warm_start
-        self._ctx = None
+        self._own: Optional[nat.OwnedContext] = None
         self._prev_solution: Optional[np.ndarray] = None
         self._prev_states: Optional[np.ndarray] = None
         self._step_count = 0
@@ -114,17 +114,25 @@ class MPCController:
     def _context(self):
         if not self.warm_start:
             return None
-        if self._ctx is None:
-            self._ctx = nat.own_context(self.device)
-            nat.check(nat.load().rmpc_ctx_set_warm_start(self._ctx, 1), "rmpc_ctx_set_warm_start")
-        return self._ctx
+        if self._own is None:
+            self._own = nat.OwnedContext(self.device)     # released by its finalizer, once
+            nat.check(nat.load().rmpc_ctx_set_warm_start(self._own.h, 1), "rmpc_ctx_set_warm_start")
+        return self._own.h
 
-    def __del__(self):
-        ctx, self._ctx = getattr(self, "_ctx", None), None
-        try:
-            nat.release_context(ctx)
-        except Exception:   # noqa: BLE001  (interpreter shutdown)
-            pass
+    def __copy__(self):
+        # a copy starts cold on a context of its own (never the original's handle)
+        c = self.__class__.__new__(self.__class__)
+        c.__dict__.update(self.__dict__)
+        c._own = None
+        return c
+
+    def __deepcopy__(self, memo):
+        import copy
+        c = self.__class__.__new__(self.__class__)
+        memo[id(self)] = c
+        for k, v in self.__dict__.items():
+            c.__dict__[k] = None if k == "_own" else copy.deepcopy(v, memo)
+        return c
 
     # -------------------------------------------------------------- single robot
     def _one(self, x0, x_refs, u_refs, obstacles, soft, ltv):
@@ -210,8 +218,8 @@ class MPCController:
         self._step_count = 0
         self._prev_solution = None
         self._prev_states = None
-        if self._ctx is not None:           # cold sets again (reset: mpc_controller.py:548-552)
-            nat.check(nat.load().rmpc_ctx_set_warm_start(self._ctx, 1), "rmpc_ctx_set_warm_start")
+        if self._own is not None:           # cold sets again (reset: mpc_controller.py:548-552)
+            nat.check(nat.load().rmpc_ctx_set_warm_start(self._own.h, 1), "rmpc_ctx_set_warm_start")
 
     def _clip_control(self, u: np.ndarray) -> np.ndarray:
         return np.array([np.clip(u[0], -self.v_max, self.v_max),

@@ -1,7 +1,7 @@
 #!/bin/bash
 export RMPC_DIAG=1   # the library reads its A/B knobs in diagnostics mode only
 # A/B of settings over one bench line (the only A/B driver): each variant is a set of
-# environment assignments -- library knobs (RMPC_FAST_CAP=9, RMPC_FAST_SPLIT=1, ...) or an
+# environment assignments -- library knobs (RMPC_FAST_CAP=9, RMPC_GROUP_GRID=2048, ...) or an
 # alternative library build (RMPC_LIB_PATH=$PWD/.../librmpc_<name>.so from build_variant.sh)
 # -- or "-" for the defaults.  Prints one line per run: value, ms/step, per-stage device times,
 # solver statistics and the parity against the C port on the timed batch.

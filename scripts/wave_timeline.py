@@ -1,0 +1,236 @@
+"""Per-wave timeline of the MPC pipeline in flight (diagnostics; needs the wave-log build:
+bash scripts/build_variant.sh wlog -DRMPC_WAVE_LOG=1).
+
+Runs BASELINE config 3 exactly as bench.py's timed loop does (S fleets in flight on their own
+contexts and streams, the in-flight stage caps, side streams off), logs every wave of the
+stage-1, tail and generic kernels for K steps (start, end, SIMD, dispatch), then the same for one
+batch alone (library default caps, launches back to back), and reports
+  - per kernel: waves, duration percentiles, SIMD-time;
+  - per SIMD: busy fraction of the window (union of its waves' intervals), the idle gaps and
+    what ran before / after each gap;
+  - per stage-1 dispatch: span, waves, and when its first / last wave started relative to the
+    previous stage-1 dispatch's end.
+Usage: RMPC_DIAG=1 RMPC_LIB_PATH=$PWD/<pkg>/rmpc/librmpc_wlog.so python scripts/wave_timeline.py
+       [--steps K] [--inflight S] [--caps F,T] [--out gpurun_out/wl.npz]"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "risk-aware-hybrid-lqr-mpc-navigation-for-autonomous-systems_amd"))
+
+import numpy as np  # noqa: E402
+
+KNAME = {1: "fast", 2: "group", 3: "solve"}
+
+
+def decode(rec):
+    kid = (rec[:, 0] >> 32).astype(np.int64)
+    blk = (rec[:, 0] & 0xffffffff).astype(np.int64)
+    t0, t1 = rec[:, 1].astype(np.int64), rec[:, 2].astype(np.int64)
+    hw = (rec[:, 3] & 0xffffffff).astype(np.int64)
+    xcc = ((rec[:, 3] >> 32) & 0xff).astype(np.int64)
+    disp = (rec[:, 3] >> 40).astype(np.int64)      # dispatch packet address bits (reused by the ring)
+    # gfx9 HW_ID: simd [5:4], cu [11:8], sh [12], se [15:13]
+    simd_key = (xcc << 16) | (hw & 0xff30)
+    return dict(kid=kid, blk=blk, t0=t0, t1=t1, simd=simd_key, disp=disp)
+
+
+def dispatches(d, kid):
+    """Kernel kid's records grouped by launch: same packet address, split where a block index
+    repeats (the queue ring reuses packet slots); in launch-start order."""
+    m = np.nonzero(d["kid"] == kid)[0]
+    out = {}
+    for i in m[np.argsort(d["t0"][m], kind="stable")]:
+        out.setdefault(int(d["disp"][i]), []).append(i)
+    res = []
+    for lst in out.values():
+        cur, seen = [], set()
+        for i in lst:
+            b = int(d["blk"][i])
+            if b in seen:
+                res.append(np.asarray(cur))
+                cur, seen = [], set()
+            cur.append(i)
+            seen.add(b)
+        if cur:
+            res.append(np.asarray(cur))
+    res.sort(key=lambda ix: d["t0"][ix].min())
+    return res
+
+
+def analyse(d, us_per_tick, label):
+    t_lo, t_hi = d["t0"].min(), d["t1"].max()
+    win = (t_hi - t_lo) * us_per_tick
+    simds = np.unique(d["simd"])
+    rep = {"label": label, "window_us": win, "waves": int(d["kid"].size), "simds_seen": int(simds.size)}
+    dur = (d["t1"] - d["t0"]) * us_per_tick
+    for k, name in KNAME.items():
+        m = d["kid"] == k
+        if not m.any():
+            continue
+        x = dur[m]
+        rep[name] = {"waves": int(m.sum()), "simd_us": float(x.sum()),
+                     "simd_frac": float(x.sum() / (simds.size * win)),
+                     "dur_us_p10_50_90_max": [round(float(np.percentile(x, q)), 2) for q in (10, 50, 90)] + [round(float(x.max()), 2)]}
+        if name == "group":
+            short = x < 2.0
+            rep[name]["empty_waves(<2us)"] = int(short.sum())
+            rep[name]["empty_simd_us"] = float(x[short].sum())
+    # per-SIMD union of busy intervals and the idle gaps between them (inside the window)
+    busy, gaps, gap_kinds, conc = 0.0, [], {}, []
+    order = np.argsort(d["simd"] * 0 + d["t0"], kind="stable")
+    by_simd = {}
+    for i in order:
+        by_simd.setdefault(int(d["simd"][i]), []).append(i)
+    for s, lst in by_simd.items():
+        cur_end, cur_kid, start = None, None, None
+        for i in lst:
+            a, b = d["t0"][i], d["t1"][i]
+            if cur_end is None:
+                start, cur_end, cur_kid = a, b, d["kid"][i]
+                if a > t_lo:
+                    gaps.append((a - t_lo) * us_per_tick)
+                    gap_kinds["start->" + KNAME[int(d["kid"][i])]] = gap_kinds.get("start->" + KNAME[int(d["kid"][i])], 0) + (a - t_lo) * us_per_tick
+                continue
+            if a > cur_end:
+                busy += (cur_end - start) * us_per_tick
+                g = (a - cur_end) * us_per_tick
+                gaps.append(g)
+                key = KNAME[int(cur_kid)] + "->" + KNAME[int(d["kid"][i])]
+                gap_kinds[key] = gap_kinds.get(key, 0.0) + g
+                start, cur_end, cur_kid = a, b, d["kid"][i]
+            else:
+                conc.append(1)
+                if b > cur_end:
+                    cur_end, cur_kid = b, d["kid"][i]
+        busy += (cur_end - start) * us_per_tick
+        if cur_end < t_hi:
+            gap_kinds[KNAME[int(cur_kid)] + "->end"] = gap_kinds.get(KNAME[int(cur_kid)] + "->end", 0.0) + (t_hi - cur_end) * us_per_tick
+    rep["simd_busy_frac"] = float(busy / (len(by_simd) * win))
+    rep["overlapping_waves_on_a_simd"] = len(conc)
+    g = np.asarray(gaps) if gaps else np.zeros(1)
+    rep["gaps"] = {"count": int(len(gaps)), "sum_simd_us": float(g.sum()), "p50_us": float(np.median(g)),
+                   "p90_us": float(np.percentile(g, 90)), "max_us": float(g.max())}
+    rep["idle_simd_us_by_transition"] = {k: round(v, 1) for k, v in sorted(gap_kinds.items(), key=lambda kv: -kv[1])}
+    # stage-1 dispatches: span and how they follow each other
+    fd = dispatches(d, 1)
+    rows = []
+    prev_end = None
+    for ix in fd:
+        a, b = d["t0"][ix].min(), d["t1"][ix].max()
+        starts = np.sort(d["t0"][ix])
+        ends = np.sort(d["t1"][ix])
+        rows.append({"waves": int(ix.size), "span_us": round((b - a) * us_per_tick, 1),
+                     "start_us": round((a - t_lo) * us_per_tick, 1),
+                     "half_waves_started_us": round((starts[ix.size // 2] - a) * us_per_tick, 1),
+                     "all_started_us": round((starts[-1] - a) * us_per_tick, 1),
+                     "half_waves_ended_us": round((ends[ix.size // 2] - a) * us_per_tick, 1),
+                     "after_prev_end_us": None if prev_end is None else round((a - prev_end) * us_per_tick, 1)})
+        prev_end = b
+    rep["fast_dispatches"] = len(rows)
+    if rows:
+        sp = np.asarray([r["span_us"] for r in rows])
+        rep["fast_span_us_mean"] = float(sp.mean())
+        rep["fast_dispatch_rows_first"] = rows[:6]
+        rep["fast_dispatch_interval_us_mean"] = float(np.mean(np.diff([r["start_us"] for r in rows]))) if len(rows) > 1 else None
+    gd = dispatches(d, 2)
+    if gd:
+        rep["group_dispatches"] = len(gd)
+        rep["group_span_us_mean"] = float(np.mean([(d["t1"][ix].max() - d["t0"][ix].min()) * us_per_tick for ix in gd]))
+        rep["group_waves_per_dispatch"] = float(np.mean([ix.size for ix in gd]))
+    return rep
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--inflight", type=int, default=3)
+    ap.add_argument("--caps", default="9,4")
+    ap.add_argument("--out", default="gpurun_out/wl.npz")
+    ap.add_argument("--cap-records", type=int, default=1 << 23)
+    args = ap.parse_args()
+    import torch
+    import rmpc
+    from rmpc import workloads as W
+    lib = rmpc._native.load()
+    lib.rmpc_diag_wlog_begin.argtypes = [C.c_uint32]
+    lib.rmpc_diag_wlog_end.argtypes = [C.c_void_p, C.c_uint32]
+    lib.rmpc_diag_wlog_end.restype = C.c_int64
+    dev = torch.device("cuda:0")
+    cfg = W.CONFIGS["cfg3"]
+    N, obs_list, seed, B = cfg["N"], cfg["obs"], cfg["seed"], cfg["B"]
+    idx = np.arange(B)
+    S = args.inflight
+    fleets, outs, counts = [], [], []
+    for f in range(S):
+        xr, ur = rmpc.batch.figure8_batch(W.fleet_t0(idx, B, f, S), N + 1, device=0)
+        x0 = xr[:, 0] + W.noise_at(idx, W.fleet_seed(seed, f))
+        fleets.append([torch.from_numpy(a).to(dev) for a in (x0, xr, ur)])
+        outs.append(dict(u0=torch.empty(B, 2, dtype=torch.float64, device=dev),
+                         u_seq=torch.empty(B, N, 2, dtype=torch.float64, device=dev),
+                         x_pred=torch.empty(B, N + 1, 3, dtype=torch.float64, device=dev),
+                         cost=torch.empty(B, dtype=torch.float64, device=dev),
+                         status=torch.empty(B, dtype=torch.int32, device=dev),
+                         slack_used=torch.empty(B, dtype=torch.uint8, device=dev),
+                         iters=torch.empty(B, dtype=torch.int32, device=dev)))
+        counts.append(torch.full((B,), 10, dtype=torch.int32, device=dev))
+    obs = torch.tensor(obs_list, dtype=torch.float64, device=dev).reshape(-1, 3)
+    p = rmpc._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(S - 1)]
+    caps = tuple(int(v) for v in args.caps.split(",")) if S > 1 else (0, 0)
+    for i in range(S):
+        rmpc.batch.set_stage_caps(*caps, device=0, slot=i)
+        rmpc.batch.set_side_stream(S == 1, device=0, slot=i)
+
+    def step(k):
+        i = k % S
+        x0, xr, ur = fleets[i]
+        rmpc.batch.mpc_solve_batch_dev(p, x0, xr, ur, obs, outs[i], step_count=counts[i], device=0,
+                                       stream=streams[i], slot=i)
+
+    reports = {}
+    host = np.zeros((args.cap_records, 4), np.uint64)
+    saved = {}
+    for label, nsteps, slots in (("inflight", args.steps, S), ("alone_default_caps", args.steps, 1)):
+        if label.startswith("alone"):
+            rmpc.batch.set_stage_caps(0, 0, device=0, slot=0)
+            rmpc.batch.set_side_stream(True, device=0, slot=0)
+        run = (lambda k: step(k)) if slots > 1 else (lambda k: step(0))
+        for k in range(max(args.warmup, S)):
+            run(k)
+        torch.cuda.synchronize()
+        assert lib.rmpc_diag_wlog_begin(args.cap_records) == 0
+        t = time.perf_counter()
+        for k in range(nsteps):
+            run(k)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t
+        n = lib.rmpc_diag_wlog_end(host.ctypes.data, args.cap_records)
+        assert n >= 0, f"wave log overflow or error ({n}): raise --cap-records"
+        rec = host[:n].copy()
+        d = decode(rec)
+        span_ticks = d["t1"].max() - d["t0"].min()
+        # s_memrealtime is 100 MHz on MI300-class parts; cross-check against the host wall clock
+        us_per_tick = 0.01
+        rep = analyse(d, us_per_tick, label)
+        rep["host_wall_us"] = wall * 1e6
+        rep["records"] = int(n)
+        rep["wall_over_span"] = wall * 1e6 / (span_ticks * us_per_tick)
+        rep["solves_per_s_from_span"] = B * nsteps / (span_ticks * us_per_tick * 1e-6)
+        st, its = outs[0]["status"].cpu().numpy(), outs[0]["iters"].cpu().numpy()
+        rep["solver"] = {"optimal": int((st == 0).sum()), "iters_mean": float(its.mean()), "iters_max": int(its.max())}
+        reports[label] = rep
+        saved[label] = rec
+        print(json.dumps(rep), flush=True)
+    os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
+    np.savez_compressed(args.out, **saved)
+
+
+if __name__ == "__main__":
+    main()

@@ -785,19 +785,15 @@ def test_simulation_drop_ins_match_logs_and_oracle(rm, golden, tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("N,obs_kind", [(30, "union8"), (20, "default")])
-@pytest.mark.parametrize("stage", ["pipeline", "fp32_sets_only", "dense_only", "generic_only"])
+@pytest.mark.parametrize("stage", ["pipeline", "dense_only", "generic_only"])
 def test_mpc_fp32_config4_accuracy(rm, capsys, monkeypatch, N, obs_kind, stage):
     """BASELINE config 4 arithmetic (fp32; N=30, 8 obstacles) against the fp64 C port on the
     same inputs: the achieved control error is measured and reported ("report
     achieved relative error honestly").  Each stage of the fp32 pipeline is also run alone:
     the default pipeline (fp32 lane-per-robot pass, fp64 refinement of its certified sets,
-    fp64 lane-group tail), the fp32 pass writing its own outputs (RMPC_NO_REFINE, the round-2
-    pipeline), every robot through the tail (RMPC_FAST_CAP=0), and the fp32 generic kernel
-    (RMPC_DISABLE_FAST)."""
-    if stage == "fp32_sets_only":
-        monkeypatch.setenv("RMPC_DIAG", "1")
-        monkeypatch.setenv("RMPC_NO_REFINE", "1")
-    elif stage == "dense_only":
+    fp64 lane-group tail), every robot through the tail (RMPC_FAST_CAP=0), and the fp32 generic
+    kernel (RMPC_DISABLE_FAST)."""
+    if stage == "dense_only":
         monkeypatch.setenv("RMPC_DIAG", "1")   # knobs are read in diagnostics mode only
         monkeypatch.setenv("RMPC_FAST_CAP", "0")
     elif stage == "generic_only":

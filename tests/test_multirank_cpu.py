@@ -178,26 +178,29 @@ def _bench(args, env=None, timeout=240):
                           capture_output=True, text=True, timeout=timeout)
 
 
-@pytest.mark.timeout(300)
-def test_bench_launcher_spawns_ranks_and_gathers(tmp_path):
-    """`python bench.py --gpus 2` with no launcher starts its own two ranks (bench.spawn_ranks:
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("world,per_rank", [(2, 512), (8, 256)])
+def test_bench_launcher_spawns_ranks_and_gathers(tmp_path, world, per_rank):
+    """`python bench.py --gpus N` with no launcher starts its own N ranks (bench.spawn_ranks:
     child processes with RANK / WORLD_SIZE / MASTER_*), here through the CPU self-test mode
     (gloo, the C port in place of the device solve; the same timing loop, aggregate and
-    gather_interleaved as the GPU run).  Exactly one JSON line comes back, with n_gpus 2 and the
-    gathered leg; the gathered u0 is bit-identical to one process solving the whole batch."""
+    gather_interleaved as the GPU run).  Exactly one JSON line comes back, with n_gpus N and the
+    gathered leg; the gathered u0 is bit-identical to one process solving the whole batch.
+    N = 8 is the driver's scaling node (BASELINE config 4): the launcher, the
+    timing collectives and the 8-way interleaved gather run at the real rank count."""
     import json
     from oracle import cpu, figure8
     out = tmp_path / "u0.npy"
-    r = _bench(["--gpus", "2", "--selftest", "--selftest-batch", "512", "--steps", "2", "--warmup", "1",
-                "--selftest-out", str(out)])
+    r = _bench(["--gpus", str(world), "--selftest", "--selftest-batch", str(per_rank), "--steps", "2",
+                "--warmup", "1", "--selftest-out", str(out)], timeout=360)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
-    assert line["n_gpus"] == 2 and line["selftest"] is True
+    assert line["n_gpus"] == world and line["selftest"] is True
     assert line["value"] > 0 and line["value_with_gather"] > 0
-    assert line["config"]["global_batch"] == 1024 and line["solver"]["optimal"] == 1024
-    B_total, N = 1024, 20
+    B_total, N = world * per_rank, 20
+    assert line["config"]["global_batch"] == B_total and line["solver"]["optimal"] == B_total
     idx = np.arange(B_total)
     xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, W.t0_at(idx, B_total), N + 1)
     x0 = xr[:, 0] + W.noise_at(idx, W.CONFIGS["cfg3"]["seed"])
