@@ -528,6 +528,18 @@ static void flip_counts(RmpcCtx *c) {
 // it does not certify within its PDAS cap go to the lane-group tail, and what
 // that one hands on (non-finite data -> fallback law, uncertified) to the generic kernel.
 // Otherwise the generic kernel alone.
+size_t rmpc_kernel_static_lds(const void *fn) {
+    static std::mutex mu;
+    static std::vector<std::pair<const void *, size_t>> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    for (const auto &e : cache)
+        if (e.first == fn) return e.second;
+    hipFuncAttributes at;
+    const size_t v = hipFuncGetAttributes(&at, fn) == hipSuccess ? at.sharedSizeBytes : RMPC_LDS_SLOT;
+    cache.emplace_back(fn, v);
+    return v;
+}
+
 static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const double *x0,
                       const double *x_refs, int32_t ref_rows, const double *u_refs, int32_t uref_rows,
                       const double *obstacles, int32_t n_obs, int32_t *step_count, double *u0,

@@ -86,6 +86,25 @@ struct MpcFastArgs {
     int prev_shift;
     uint32_t prev_stamp;
 };
+// LDS slot.  The LDS-using kernels of the MPC pipeline (the lane-per-robot stage, the lane-group
+// tail, the generic kernel's leftover list) each run one wave per SIMD, four per CU, and with
+// batches in flight they replace each other on the CUs.  A CU allocates each workgroup's LDS as
+// one contiguous range, so a tail workgroup (37.6 KB) leaving a hole smaller than a stage
+// workgroup (39.8 KB) kept the next stage wave off that SIMD, and a 121-KB generic workgroup
+// could start only on an emptied CU.  Every such workgroup requests exactly one quarter of the
+// CU's LDS instead (static + dynamic = RMPC_LDS_SLOT), so any hole fits any of them.
+#define RMPC_LDS_SLOT (160 * 1024 / 4)
+// static LDS bytes of a kernel (hipFuncGetAttributes, cached)
+size_t rmpc_kernel_static_lds(const void *fn);
+// the dynamic LDS to request: `need` padded up to the slot when the kernel takes most of one
+// (at least 3/4: those instances are also the one-wave-per-SIMD ones; a smaller request, e.g.
+// the fp32 N = 20 stage's 24 KB at 207 VGPRs, keeps its higher occupancy)
+static inline size_t rmpc_lds_slot_pad(const void *fn, size_t need) {
+    const size_t st = rmpc_kernel_static_lds(fn);
+    return (need + st <= RMPC_LDS_SLOT && 4 * (need + st) >= 3 * RMPC_LDS_SLOT) ? RMPC_LDS_SLOT - st : need;
+}
+
+
 // list counters per set of a context (retry_count holds two sets, used by alternate calls)
 #define RMPC_COUNT_WORDS 16
 

@@ -620,7 +620,8 @@ __device__ __forceinline__ void mpc_solve_one(const MpcArgs<T> &a, int64_t t) {
     if (a.iters) a.iters[b] = it;
 }
 
-// USE_LDS (the small retry lists after the tails): a grid of at most one workgroup per CU
+#define GENERIC_GRID_MAX 16
+// USE_LDS (the small retry lists after the tails): a grid of GENERIC_GRID_MAX workgroups
 // looping over the list, so an empty or short list does not dispatch capacity / lanes
 // workgroups that each hold 128 KB of LDS only to exit
 template <typename T, bool USE_LDS>
@@ -668,11 +669,17 @@ MpcLayout rmpc_mpc_layout(int N, int bs, int no) {
     return L;
 }
 
+// Lanes per workgroup of the LDS generic kernel (the leftover list after the tails): as many
+// robots as fit one LDS slot (RMPC_LDS_SLOT) -- the list is short, and a workgroup that needs a
+// whole CU's LDS starts only where every other workgroup has left (RMPC_LDS_SLOT) -- else as
+// many as fit the CU.
 int rmpc_mpc_lds_lanes(const MpcLayout &L) {
     const size_t per_lane = (size_t)L.REC * sizeof(double);
-    const size_t cap = 160 * 1024;
     int lanes = 64;
-    while (lanes > 0 && (size_t)lanes * per_lane > cap) lanes >>= 1;
+    while (lanes > 0 && (size_t)lanes * per_lane > RMPC_LDS_SLOT) lanes >>= 1;
+    if (lanes > 0) return lanes;
+    lanes = 64;
+    while (lanes > 0 && (size_t)lanes * per_lane > 160 * 1024) lanes >>= 1;
     return lanes;
 }
 
@@ -699,7 +706,7 @@ static hipError_t launch_generic(const MpcDevParams &prm, const MpcLayout &L, in
     a.zero_next = zero_next;
     if (B <= 0) return hipSuccess;
     if (lds_lanes > 0) {
-        const size_t lds = (size_t)L.REC * lds_lanes * sizeof(T);
+        const size_t lds = rmpc_lds_slot_pad((const void *)mpc_solve_kernel<T, true>, (size_t)L.REC * lds_lanes * sizeof(T));
         // the attribute is per device: one bit per device that has it (contexts on several
         // GPUs may share a process)
         static std::atomic<unsigned long long> attr_set{0};
@@ -718,7 +725,11 @@ static hipError_t launch_generic(const MpcDevParams &prm, const MpcLayout &L, in
             if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
             n_cu.store(v);
         }
-        int64_t blocks = (B + lds_lanes - 1) / lds_lanes;
+        // a few workgroups looping over the (short) list: each one has to find a free LDS slot
+        // in flight (RMPC_GENERIC_GRID=<workgroups>: another cap, A/B)
+        int64_t blocks = (B + lds_lanes - 1) / lds_lanes, cap = GENERIC_GRID_MAX;
+        if (const char *g = rmpc_knob("RMPC_GENERIC_GRID")) cap = atoll(g) > 0 ? atoll(g) : cap;
+        if (blocks > cap) blocks = cap;
         if (blocks > n_cu.load()) blocks = n_cu.load();
         hipLaunchKernelGGL((mpc_solve_kernel<T, true>), dim3((unsigned)blocks), dim3(lds_lanes), lds,
                            stream, a);

@@ -56,31 +56,34 @@ hipError_t rmpc_launch_mpc_fast(const MpcFastArgs &a, int N, int bs, int prec, h
                        (size_t)RMPC_WAVE * 17 * sizeof(double);
     const size_t lds2 = (size_t)3 * N * (RMPC_WAVE / 2) * (prec == RMPC_F32 ? sizeof(float) : sizeof(double)) +
                         (size_t)(RMPC_WAVE / 2) * 17 * sizeof(double);
+    // every launch requests one LDS slot (rmpc_lds_slot_pad, RMPC_LDS_SLOT)
+#define FK(kern, g, need) hipLaunchKernelGGL(kern, g, block, rmpc_lds_slot_pad((const void *)kern, need), stream, a)
     if (lti) {
         if (prec == RMPC_F32) return hipErrorInvalidValue;
-        if (N == 20 && a.no == 3) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, true, 3>), grid, block, lds, stream, a);
-        else if (N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, true>), grid, block, lds, stream, a);
-        else if (N == 10) hipLaunchKernelGGL((mpc_ltv_fast_kernel<10, 1, double, true>), grid, block, lds, stream, a);
-        else if (N == 6) hipLaunchKernelGGL((mpc_ltv_fast_kernel<6, 1, double, true>), grid, block, lds, stream, a);
+        if (N == 20 && a.no == 3) FK((mpc_ltv_fast_kernel<20, 1, double, true, 3>), grid, lds);
+        else if (N == 20) FK((mpc_ltv_fast_kernel<20, 1, double, true>), grid, lds);
+        else if (N == 10) FK((mpc_ltv_fast_kernel<10, 1, double, true>), grid, lds);
+        else if (N == 6) FK((mpc_ltv_fast_kernel<6, 1, double, true>), grid, lds);
         else return hipErrorInvalidValue;
     } else if (prec == RMPC_F32) {
         // paired lanes for the 8-obstacle N = 30 instance
         const dim3 grid2((unsigned)((n + RMPC_WAVE / 2 - 1) / (RMPC_WAVE / 2)));
-        if (bs == 1 && N == 30 && a.no == 8) hipLaunchKernelGGL((mpc_ltv_fast_kernel<30, 1, float, false, 8, 2>), grid2, block, lds2, stream, a);
-        else if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, float, false>), grid, block, lds, stream, a);
+        if (bs == 1 && N == 30 && a.no == 8) FK((mpc_ltv_fast_kernel<30, 1, float, false, 8, 2>), grid2, lds2);
+        else if (bs == 1 && N == 20) FK((mpc_ltv_fast_kernel<20, 1, float, false>), grid, lds);
         else return hipErrorInvalidValue;
     } else {
         const dim3 grid2((unsigned)((n + RMPC_WAVE / 2 - 1) / (RMPC_WAVE / 2)));
         // (N = 30, 8 obstacles in fp64: paired lanes -- fp64 requests and the fp32 requests'
         // refinement pass)
-        if (bs == 1 && N == 30 && a.no == 8) hipLaunchKernelGGL((mpc_ltv_fast_kernel<30, 1, double, false, 8, 2>), grid2, block, lds2, stream, a);
-        else if (bs == 1 && N == 20 && a.no == 3 && a.prev_sets) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, false, 3>), grid, block, lds, stream, a);
-        else if (bs == 1 && N == 20 && a.no == 3) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, false, 3, 1, false>), grid, block, lds, stream, a);
-        else if (bs == 1 && N == 20) hipLaunchKernelGGL((mpc_ltv_fast_kernel<20, 1, double, false>), grid, block, lds, stream, a);
-        else if (bs == 1 && N == 10) hipLaunchKernelGGL((mpc_ltv_fast_kernel<10, 1, double, false>), grid, block, lds, stream, a);
-        else if (bs == 1 && N == 6) hipLaunchKernelGGL((mpc_ltv_fast_kernel<6, 1, double, false>), grid, block, lds, stream, a);
-        else if (bs == 2 && N == 6) hipLaunchKernelGGL((mpc_ltv_fast_kernel<6, 2, double, false>), grid, block, lds, stream, a);
+        if (bs == 1 && N == 30 && a.no == 8) FK((mpc_ltv_fast_kernel<30, 1, double, false, 8, 2>), grid2, lds2);
+        else if (bs == 1 && N == 20 && a.no == 3 && a.prev_sets) FK((mpc_ltv_fast_kernel<20, 1, double, false, 3>), grid, lds);
+        else if (bs == 1 && N == 20 && a.no == 3) FK((mpc_ltv_fast_kernel<20, 1, double, false, 3, 1, false>), grid, lds);
+        else if (bs == 1 && N == 20) FK((mpc_ltv_fast_kernel<20, 1, double, false>), grid, lds);
+        else if (bs == 1 && N == 10) FK((mpc_ltv_fast_kernel<10, 1, double, false>), grid, lds);
+        else if (bs == 1 && N == 6) FK((mpc_ltv_fast_kernel<6, 1, double, false>), grid, lds);
+        else if (bs == 2 && N == 6) FK((mpc_ltv_fast_kernel<6, 2, double, false>), grid, lds);
         else return hipErrorInvalidValue;
     }
+#undef FK
     return hipGetLastError();
 }

@@ -161,7 +161,7 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
         }
     }
     a.pdas_cap = pdas_cap < RMPC_PDAS_ITERS ? pdas_cap : RMPC_PDAS_ITERS;
-    const size_t lds = (size_t)rpw * group_rec_bytes(N, bs, no, false);
+    size_t lds = (size_t)rpw * group_rec_bytes(N, bs, no, false);
     const dim3 g((unsigned)grid), blk(64);
 #define GK(n, b, g, t, l) (const void *)mpc_group_kernel<n, b, g, t, l>
     const void *fn = (bs == 1 && N == 30)   ? (lti ? GK(30, 1, 32, double, true) : GK(30, 1, 32, double, false))
@@ -170,6 +170,7 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
                      : (bs == 1 && N == 6)  ? (lti ? GK(6, 1, 16, double, true) : GK(6, 1, 16, double, false))
                                             : GK(6, 2, 16, double, false);
 #undef GK
+    lds = rmpc_lds_slot_pad(fn, lds);          // one LDS slot (RMPC_LDS_SLOT)
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

@@ -44,6 +44,11 @@ __device__ __forceinline__ unsigned wl_take() {
 // at the wave's end (every lane calls; lane 0 writes)
 __device__ __forceinline__ void wl_record(int kid, unsigned slot, unsigned long long t0) {
     if (threadIdx.x != 0 || slot == ~0u) return;
+#if RMPC_WLOG_DRAIN
+    // (variant: the end after the wave's outstanding memory operations -- its last stores --
+    // have completed, which the SIMD's release waits for)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
     const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_REG_HW_ID
     const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
