@@ -343,13 +343,9 @@ def main():
                     help="A/B: order each fleet's robots by predicted difficulty within blocks of this size")
     ap.add_argument("--inflight-side", action="store_true",
                     help="keep the library's side streams on the in-flight contexts (A/B; default off there)")
-    ap.add_argument("--inflight", type=int, default=3,
+    ap.add_argument("--inflight", type=int, default=8,
                     help="MPC configs: batches in flight at once, each on its own stream with its own "
                          "solver context and outputs (step k runs on stream k mod S)")
-    ap.add_argument("--wave-order", type=int, default=512,
-                    help="in-flight contexts: robots ordered into waves by predicted difficulty within blocks "
-                         "of this size (rmpc_ctx_set_wave_order; 0: input order)")
-    ap.add_argument("--wave-order-alone", action="store_true", help="A/B: the wave order with one batch in flight too")
     ap.add_argument("--hw-queues", type=int, default=16,
                     help="hardware queues per process (GPU_MAX_HW_QUEUES, at most 32; HIP's default is 4): "
                          "each batch in flight needs a queue of its own, or two fleets' streams share one "
@@ -457,10 +453,6 @@ def main():
         # streams sharing the hardware queues: off there (rmpc_ctx_set_side_stream; config 4
         # 69.9M against 66.0M solves/s, profiles/r03/ab_side_streams_in_flight.txt)
         rmpc.batch.set_side_stream(S == 1 or args.inflight_side, device=local, slot=i)
-        # in flight, waves of other batches fill the SIMDs a batch's finished waves free, so the
-        # SIMD time a wave holds is what counts: waves of similar robots hold less of it
-        # (rmpc_ctx_set_wave_order; one batch alone waits for its slowest wave either way)
-        rmpc.batch.set_wave_order(args.wave_order if S > 1 or args.wave_order_alone else 0, device=local, slot=i)
 
     def step(k=0):
         i = k % S
@@ -491,7 +483,6 @@ def main():
     # per-stage device time of that launch (separate, untimed pass: events between the
     # pipeline's kernels; only the lane-per-robot pipeline has stages)
     rmpc.batch.set_stage_caps(0, 0, device=local, slot=0)
-    rmpc.batch.set_wave_order(args.wave_order if args.wave_order_alone else 0, device=local, slot=0)
     rmpc.batch.set_stage_timing(True, device=local)
     stage = []
     try:
@@ -503,7 +494,6 @@ def main():
         stage_ms = None
     rmpc.batch.set_stage_timing(False, device=local)
     rmpc.batch.set_stage_caps(*caps, device=local, slot=0)
-    rmpc.batch.set_wave_order(args.wave_order if S > 1 or args.wave_order_alone else 0, device=local, slot=0)
 
     # N > 1: the same K steps again with the batch gather of u0 inside the timed region
     # (SURVEY 8(e)'s collective: RCCL all_gather over xGMI; the round-robin shards interleave

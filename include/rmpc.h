@@ -165,15 +165,6 @@ int rmpc_ctx_set_stage_caps(RmpcCtx *ctx, int32_t fast_cap, int32_t tail_cap);
  * to the streams sharing the device's hardware queues (GPU_MAX_HW_QUEUES), and the other
  * batches already fill the chip: the bench turns them off there (HISTORY.md section 1). */
 int rmpc_ctx_set_side_stream(RmpcCtx *ctx, int32_t on);
-/* Wave order on this context (a performance setting; results are identical): block > 0 makes
- * every whole-batch MPC call first order the robots of each block of `block` consecutive robots
- * by a predicted-difficulty key (a device kernel: the obstacle rows the start error's free
- * response violates plus the start error), and the lane-per-robot stage read them in that
- * order, so a 64-robot wave holds robots of similar PDAS iteration counts.  Outputs stay in
- * input order.  It pays with several batches in flight, whose waves fill each other's idle
- * SIMDs (config 3, 8 in flight: +7%); one batch alone waits for its slowest wave either way.
- * block: 0 (default: input order) or a multiple of 64 in [64, 1024]. */
-int rmpc_ctx_set_wave_order(RmpcCtx *ctx, int32_t block);
 /* Warm start across calls on this context (replaces the reference's warm_start=True solves
  * with get_warm_start's shifted previous solution, mpc_controller.py:272-277, 470-475,
  * 524-538).  On, every whole-batch MPC call (rmpc_mpc_solve_batch[_dev]; MPC-mode rollouts)

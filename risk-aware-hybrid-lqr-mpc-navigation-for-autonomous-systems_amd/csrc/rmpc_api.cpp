@@ -95,8 +95,6 @@ struct RmpcCtx {
     bool timed = false;
     int fast_cap = 0, tail_cap = 0;   // rmpc_ctx_set_stage_caps (0: library default)
     bool use_side = true;             // rmpc_ctx_set_side_stream
-    int wave_order = 0;               // rmpc_ctx_set_wave_order: block size (0: robots in input order)
-    DevBuf order;                     // [B + 64 + B]: the wave order (robot ids), its count, the keys
     // rmpc_ctx_set_warm_start: per-robot active sets of each robot's previous solve
     // (MpcFastArgs::prev_sets), valid for the batch shape warm_B / warm_key they were made for
     bool warm_on = false;
@@ -285,7 +283,6 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     c->counts.release();
     c->hyb_status.release();
     c->fast_gains.release();
-    c->order.release();
     c->retry.release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -356,15 +353,6 @@ int rmpc_ctx_set_side_stream(RmpcCtx *c, int32_t on) {
     if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
     c->use_side = on != 0;
     for (auto &sc : c->sub) sc->use_side = on != 0;
-    return RMPC_OK;
-}
-
-int rmpc_ctx_set_wave_order(RmpcCtx *c, int32_t block) {
-    if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
-    if (block != 0 && (block < 64 || block > 1024 || block % 64))
-        return fail(RMPC_EINVAL, "block %d: 0, or a multiple of 64 in [64, 1024]", block);
-    c->wave_order = block;
-    for (auto &sc : c->sub) sc->wave_order = block;
     return RMPC_OK;
 }
 
@@ -620,16 +608,6 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
         HIP_TRY(c->retry.ensure((size_t)B * sizeof(int32_t)));
         int32_t *cnt = nullptr;
         HIP_TRY(take_counts(c, s, &cnt));
-        // wave order (rmpc_ctx_set_wave_order; a whole batch only): the stage reads its robots
-        // through a per-block difficulty order, so a wave's robots need similar iteration counts
-        if (c->wave_order > 0 && !index && B >= c->wave_order) {
-            HIP_TRY(c->order.ensure((size_t)(2 * B + 64) * sizeof(int32_t)));
-            int32_t *ord = (int32_t *)c->order.p;
-            HIP_TRY(rmpc_launch_wave_order(B, p->horizon, c->wave_order, x0, x_refs, ref_rows, u_refs, uref_rows, ref_off,
-                                           obstacles, n_obs, p->d_safe, p->dt, ord + B + 64, ord, ord + B, s));
-            index = ord;
-            count = ord + B;
-        }
         MpcFastArgs a;
         memset(&a, 0, sizeof(a));
         a.prm = d;

@@ -199,12 +199,6 @@ hipError_t rmpc_launch_figure8_table(int64_t B, const int32_t *start, int32_t k,
                                      double A, double a, double dt, double *x_refs, double *u_refs,
                                      hipStream_t stream);
 hipError_t rmpc_launch_iota(int64_t B, int32_t *idx, int32_t *count, hipStream_t stream);
-// robots of each block of `blk` (a multiple of 64, <= 1024) ordered by predicted difficulty
-// into order[B] (key[B]: scratch); *count = B (rmpc_ctx_set_wave_order)
-hipError_t rmpc_launch_wave_order(int64_t B, int N, int blk, const double *x0, const double *x_refs, int ref_rows,
-                                  const double *u_refs, int uref_rows, const int32_t *ref_off, const double *obs,
-                                  int no, double d_safe, double dt, int32_t *key, int32_t *order, int32_t *count,
-                                  hipStream_t stream);
 hipError_t rmpc_launch_ref_offsets(int64_t B, const int32_t *start, int32_t k, int32_t last, int32_t *off,
                                    hipStream_t stream);
 hipError_t rmpc_launch_rollout_init(int64_t B, const int32_t *start, const double *x0, int32_t table_len,

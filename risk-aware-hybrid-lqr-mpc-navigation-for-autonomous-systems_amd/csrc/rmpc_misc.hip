@@ -301,94 +301,6 @@ __global__ __launch_bounds__(256) void status_count_kernel(int64_t B, const int3
 }
 
 
-// ---- wave order (rmpc_ctx_set_wave_order): the robots of each block of `blk` consecutive
-// robots ordered by a predicted-difficulty key, so that a 64-robot wave of the lane-per-robot
-// stage holds robots of similar PDAS iteration counts (a wave runs as many iterations as its
-// slowest robot).  Key (as rmpc.workloads.difficulty_key): the hinge rows the free response of
-// the start error under the reference inputs violates (mpc_controller.py:439-468 rows) + 8
-// |heading error| + 2 |position error|.  Two kernels of one-wave workgroups and no LDS, short:
-// in flight every wave of them holds a SIMD that another batch's stage wave could use (a first
-// version ranked a block in one 512-thread workgroup, which waited for an emptied CU).
-__global__ __launch_bounds__(64) void wave_key_kernel(int64_t B, int N, const double *x0, const double *x_refs,
-                                                      int ref_rows, const double *u_refs, int uref_rows,
-                                                      const int32_t *ref_off, const double *obs, int no, double d_safe,
-                                                      double dt, int32_t *key) {
-    // (a heuristic: fp32 arithmetic)
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
-    const double *xr = x_refs + ref_row0(ref_off, b, ref_rows) * 3;
-    const double *ur = u_refs + ref_row0(ref_off, b, uref_rows) * 2;
-    float e0 = (float)(x0[3 * b] - xr[0]), e1 = (float)(x0[3 * b + 1] - xr[1]);
-    const float e2 = (float)wrap_pi(x0[3 * b + 2] - xr[2]);
-    const float pos = sqrtf(e0 * e0 + e1 * e1), dtf = (float)dt, sf = (float)d_safe;
-    // the obstacles in registers (loaded inside the step loop, every row was a dependent
-    // memory latency)
-    float ox[RMPC_MAX_OBSTACLES], oy[RMPC_MAX_OBSTACLES], osf[RMPC_MAX_OBSTACLES];
-#pragma unroll
-    for (int o = 0; o < RMPC_MAX_OBSTACLES; o++) {
-        const bool on = o < no;
-        ox[o] = on ? (float)obs[3 * o] : 0.0f;
-        oy[o] = on ? (float)obs[3 * o + 1] : 0.0f;
-        osf[o] = on ? sf + (float)obs[3 * o + 2] : -1.0e30f;      // (absent: never violated)
-    }
-    float viol = 0.0f;
-    // steps in chunks of KC: a chunk's loads are issued together (one memory latency per chunk,
-    // not per step -- the per-step loop was latency-bound at ~1 us a step)
-    constexpr int KC = 8;
-    for (int k0 = 0; k0 < N; k0 += KC) {
-        float px[KC], py[KC], th[KC], vv[KC];
-#pragma unroll
-        for (int q = 0; q < KC; q++) {
-            const int k = k0 + q < N ? k0 + q : N - 1;
-            px[q] = (float)xr[3 * k]; py[q] = (float)xr[3 * k + 1]; th[q] = (float)xr[3 * k + 2];
-            vv[q] = (float)ur[2 * k];
-        }
-#pragma unroll
-        for (int q = 0; q < KC; q++) {
-            const int k = k0 + q;
-            if (k >= N) break;
-            if (k > 0) {
-#pragma unroll
-                for (int o = 0; o < RMPC_MAX_OBSTACLES; o++) {
-                    if (o >= no) break;
-                    // safe - n.(p + e - o) > 0 with n = d / |d|: multiplied through by |d| > 0
-                    const float dx = px[q] - ox[o], dy = py[q] - oy[o];
-                    const float dist = fmaxf(__builtin_sqrtf(dx * dx + dy * dy), 1e-12f);
-                    viol += osf[o] * dist - (dx * (dx + e0) + dy * (dy + e1)) > 0.0f ? 1.0f : 0.0f;
-                }
-            }
-            const float vr = fabsf(vv[q]) > 0.01f ? vv[q] : 0.1f;
-            float sn, cs;
-            __sincosf(th[q], &sn, &cs);
-            e0 -= vr * sn * dtf * e2;
-            e1 += vr * cs * dtf * e2;
-        }
-    }
-    // an integer key, unique in the block: the quantised score (1/64 steps) above the robot's
-    // place in the block (rank = the number of smaller keys; non-finite data: last)
-    const float kv = viol + 8.0f * fabsf(e2) + 2.0f * pos;
-    const int q = kv == kv ? (int)fminf(kv * 64.0f, 1048575.0f) : 1048575;
-    key[b] = (q << 10) | (int)(b % 1024);
-}
-
-// robot b's position in its block: the number of smaller keys (keys are unique).  The block's
-// keys come 64 at a time, one per lane (a coalesced load), and are broadcast lane by lane
-// (v_readlane): per key one compare for the whole wave, no memory latency.
-__global__ __launch_bounds__(64) void wave_rank_kernel(int64_t B, int blk, const int32_t *key, int32_t *order, int32_t *count) {
-    const int lane = threadIdx.x;
-    const int64_t b = (int64_t)blockIdx.x * 64 + lane;
-    const int64_t b0 = (int64_t)blockIdx.x * 64 / blk * blk;             // the block's first robot
-    const int n = (int)(B - b0 < blk ? B - b0 : blk);
-    const int kb = b < B ? key[b] : 0x7fffffff;
-    int rank = 0;
-    for (int c = 0; c < n; c += 64) {
-        const int kl = c + lane < n ? key[b0 + c + lane] : 0x7fffffff;   // (past the batch: never smaller)
-#pragma unroll
-        for (int q = 0; q < 64; q++) rank += __builtin_amdgcn_readlane(kl, q) < kb ? 1 : 0;
-    }
-    if (b < B) order[b0 + rank] = (int32_t)b;
-    if (b == 0) *count = (int32_t)B;
-}
 }  // namespace rmpc
 
 using namespace rmpc;
@@ -478,18 +390,5 @@ hipError_t rmpc_launch_figure8(int64_t B, const double *t0, int rows, double A, 
     if (B <= 0 || rows <= 0) return hipSuccess;
     hipLaunchKernelGGL(figure8_kernel, dim3(nblk(B * rows, 256)), dim3(256), 0, stream, B, t0, rows, A, a,
                        dt, x_refs, u_refs);
-    return hipGetLastError();
-}
-
-hipError_t rmpc_launch_wave_order(int64_t B, int N, int blk, const double *x0, const double *x_refs, int ref_rows,
-                                  const double *u_refs, int uref_rows, const int32_t *ref_off, const double *obs,
-                                  int no, double d_safe, double dt, int32_t *key, int32_t *order, int32_t *count,
-                                  hipStream_t stream) {
-    if (B <= 0) return hipSuccess;
-    if (blk < 64 || blk > 1024 || blk % 64) return hipErrorInvalidValue;
-    const dim3 g((unsigned)((B + 63) / 64));
-    hipLaunchKernelGGL(wave_key_kernel, g, dim3(64), 0, stream, B, N, x0, x_refs, ref_rows, u_refs, uref_rows, ref_off,
-                       obs, no, d_safe, dt, key);
-    hipLaunchKernelGGL(wave_rank_kernel, g, dim3(64), 0, stream, B, blk, (const int32_t *)key, order, count);
     return hipGetLastError();
 }

@@ -241,14 +241,6 @@ def set_side_stream(on=True, device=0, slot=0):
     check(lib.rmpc_ctx_set_side_stream(nat.context(device, slot), int(bool(on))), "rmpc_ctx_set_side_stream")
 
 
-def set_wave_order(block=0, device=0, slot=0):
-    """Wave order of one context (rmpc_ctx_set_wave_order): each whole-batch MPC solve orders the
-    robots of every `block` consecutive robots by predicted difficulty before the lane-per-robot
-    stage (0: input order, the default).  Same results; pays with several batches in flight."""
-    lib = nat.load()
-    check(lib.rmpc_ctx_set_wave_order(nat.context(device, slot), int(block)), "rmpc_ctx_set_wave_order")
-
-
 def set_warm_start(on=True, device=0, slot=0):
     """Warm start across calls on one context (rmpc_ctx_set_warm_start): each whole-batch MPC
     solve starts robot b's active-set iteration from robot b's previous certified sets, shifted

@@ -857,39 +857,19 @@ def test_side_stream_on_off_bitwise_identical(rm):
             np.testing.assert_array_equal(x, y)
 
 
-def test_wave_order_bitwise_identical(rm):
-    """rmpc_ctx_set_wave_order: the lane-per-robot stage reading each 512-robot block in
-    predicted-difficulty order gives bitwise the outputs of input order -- a config-3 batch whose
-    size is neither a multiple of the block nor of 64 (a partial last block and wave), and an
-    MPC rollout, whose references come from the shared table through per-robot row offsets."""
+def test_rollout_used_flag_per_mode(rm):
+    """rmpc_rollout_batch's used_mpc: every step's controller -- MPC in MPC mode, LQR in LQR mode
+    (run_simulation.py logs one controller per mode), the switch's choice in hybrid mode.  Until
+    round 5 the MPC and LQR modes left the array unwritten."""
     from rmpc import workloads as W
-    B, N = 8192 + 100, 20
-    idx = np.arange(B)
-    xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, W.t0_at(idx, B), N + 1)
-    x0 = xr[:, 0] + W.noise_at(idx, 5)
-    p = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+    N = 20
     mp = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
-    start = (idx * 7 % 600).astype(np.int32)
-    outs = {}
-    try:
-        for blk, slot in ((0, 0), (512, 6)):
-            rm.batch.set_wave_order(blk, slot=slot)
-            r = rm.batch.mpc_solve_batch(p, x0, xr, ur, W.DEFAULT_OBS, step_count=np.full(B, 10, np.int32),
-                                         slot=slot)
-            ro = rm.batch.rollout_batch("mpc", 12, mparams=mp, start_index=start[:2048], obstacles=W.DEFAULT_OBS,
-                                        mpc_rate=1, slot=slot)
-            outs[blk] = (r, ro)
-    finally:
-        rm.batch.set_wave_order(0, slot=6)
-    (r0, o0), (r1, o1) = outs[0], outs[512]
-    assert np.all(r0["status"] == 0)
-    for k in ("u0", "u_seq", "x_pred", "cost", "status", "iters", "slack_used"):
-        np.testing.assert_array_equal(r1[k], r0[k])
-    for k in ("states", "controls", "used_mpc", "mpc_status"):
-        np.testing.assert_array_equal(o1[k], o0[k])
-    assert o0["used_mpc"].all()                        # MPC mode: every step's controller is MPC
-    with pytest.raises(rm.RmpcError):
-        rm.batch.set_wave_order(100, slot=6)           # not a multiple of 64
+    lp = rm._native.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0)
+    start = (np.arange(512) * 7 % 600).astype(np.int32)
+    ro = rm.batch.rollout_batch("mpc", 8, mparams=mp, start_index=start, obstacles=W.DEFAULT_OBS, mpc_rate=1)
+    assert ro["used_mpc"].all() and ro["mpc_status"][0] == 512 * 8
+    rl = rm.batch.rollout_batch("lqr", 8, lparams=lp, start_index=start)
+    assert not rl["used_mpc"].any()
 
 
 def _closed_loop_warm_vs_cold(rm, p, B, steps, obs, seed, N, slot=3):
