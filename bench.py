@@ -346,6 +346,8 @@ def main():
     ap.add_argument("--inflight", type=int, default=8,
                     help="MPC configs: batches in flight at once, each on its own stream with its own "
                          "solver context and outputs (step k runs on stream k mod S)")
+    ap.add_argument("--cold-start", type=int, default=1, choices=[0, 1],
+                    help="in-flight contexts' first active sets (rmpc_ctx_set_cold_start): 1 zero-correction rows")
     ap.add_argument("--hw-queues", type=int, default=16,
                     help="hardware queues per process (GPU_MAX_HW_QUEUES, at most 32; HIP's default is 4): "
                          "each batch in flight needs a queue of its own, or two fleets' streams share one "
@@ -453,6 +455,9 @@ def main():
         # streams sharing the hardware queues: off there (rmpc_ctx_set_side_stream; config 4
         # 69.9M against 66.0M solves/s, profiles/r03/ab_side_streams_in_flight.txt)
         rmpc.batch.set_side_stream(S == 1 or args.inflight_side, device=local, slot=i)
+        # in flight the total PDAS work sets the rate, not the hardest robot's chain: the
+        # zero-correction first sets (rmpc_ctx_set_cold_start)
+        rmpc.batch.set_cold_start(args.cold_start if S > 1 else 0, device=local, slot=i)
 
     def step(k=0):
         i = k % S
@@ -483,6 +488,7 @@ def main():
     # per-stage device time of that launch (separate, untimed pass: events between the
     # pipeline's kernels; only the lane-per-robot pipeline has stages)
     rmpc.batch.set_stage_caps(0, 0, device=local, slot=0)
+    rmpc.batch.set_cold_start(0, device=local, slot=0)
     rmpc.batch.set_stage_timing(True, device=local)
     stage = []
     try:
@@ -494,6 +500,7 @@ def main():
         stage_ms = None
     rmpc.batch.set_stage_timing(False, device=local)
     rmpc.batch.set_stage_caps(*caps, device=local, slot=0)
+    rmpc.batch.set_cold_start(args.cold_start if S > 1 else 0, device=local, slot=0)
 
     # N > 1: the same K steps again with the batch gather of u0 inside the timed region
     # (SURVEY 8(e)'s collective: RCCL all_gather over xGMI; the round-robin shards interleave
@@ -983,6 +990,7 @@ def bench_other(args, world, rank, local, dist, pre=None):
             rmpc.batch.set_stage_caps(*caps, device=local, slot=i)
             # (config 5 keeps its side stream in flight: 398-418M against 233M steps/s without)
             rmpc.batch.set_side_stream(True, device=local, slot=i)
+            rmpc.batch.set_cold_start(args.cold_start if S > 1 else 0, device=local, slot=i)
 
         def step(k=0):
             i = k % S
@@ -1000,8 +1008,10 @@ def bench_other(args, world, rank, local, dist, pre=None):
         # one batch alone with the library's default caps (what one batch at a time would use)
         torch.cuda.synchronize()
         rmpc.batch.set_stage_caps(0, 0, device=local, slot=0)
+        rmpc.batch.set_cold_start(0, device=local, slot=0)
         alone_default_s = alone_times(lambda: step(0), torch.cuda.current_stream(), args.steps)[0] / 1e3
         rmpc.batch.set_stage_caps(*caps, device=local, slot=0)
+        rmpc.batch.set_cold_start(args.cold_start if S > 1 else 0, device=local, slot=0)
     k_roof_s = alone_default_s or k_avg_s     # the roofline's launch: one batch alone, library defaults
     elapsed, _ = W.aggregate(dist, elapsed, [], device=coll_device(args, dev))
     line = {"metric": metric, "value": B_total * args.steps / elapsed,

@@ -165,6 +165,14 @@ int rmpc_ctx_set_stage_caps(RmpcCtx *ctx, int32_t fast_cap, int32_t tail_cap);
  * to the streams sharing the device's hardware queues (GPU_MAX_HW_QUEUES), and the other
  * batches already fill the chip: the bench turns them off there (HISTORY.md section 1). */
 int rmpc_ctx_set_side_stream(RmpcCtx *ctx, int32_t on);
+/* First active sets of a cold solve on this context (a performance setting; the QP and its
+ * optimum are unchanged): 0 (default) starts every robot's PDAS from empty sets; 1 starts the
+ * hinge rows that the start error's free response under the reference inputs violates active
+ * (mpc_controller.py:439-468 rows).  Mode 1 lowers the PDAS work per robot (config 3: mean
+ * iterations 2.18 -> 2.02, robots handed to the tail 3552 -> 2211) but lengthens the hardest
+ * robots' chains: with batches in flight it pays (configs 4 / 5: +4%), one batch alone it
+ * costs ~10% (HISTORY.md).  Warm-started solves (rmpc_ctx_set_warm_start) are unaffected. */
+int rmpc_ctx_set_cold_start(RmpcCtx *ctx, int32_t mode);
 /* Warm start across calls on this context (replaces the reference's warm_start=True solves
  * with get_warm_start's shifted previous solution, mpc_controller.py:272-277, 470-475,
  * 524-538).  On, every whole-batch MPC call (rmpc_mpc_solve_batch[_dev]; MPC-mode rollouts)

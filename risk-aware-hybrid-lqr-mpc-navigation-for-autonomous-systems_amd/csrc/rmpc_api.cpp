@@ -95,6 +95,7 @@ struct RmpcCtx {
     bool timed = false;
     int fast_cap = 0, tail_cap = 0;   // rmpc_ctx_set_stage_caps (0: library default)
     bool use_side = true;             // rmpc_ctx_set_side_stream
+    bool cold_rows = false;           // rmpc_ctx_set_cold_start: 1 = zero-correction rows active
     // rmpc_ctx_set_warm_start: per-robot active sets of each robot's previous solve
     // (MpcFastArgs::prev_sets), valid for the batch shape warm_B / warm_key they were made for
     bool warm_on = false;
@@ -353,6 +354,14 @@ int rmpc_ctx_set_side_stream(RmpcCtx *c, int32_t on) {
     if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
     c->use_side = on != 0;
     for (auto &sc : c->sub) sc->use_side = on != 0;
+    return RMPC_OK;
+}
+
+int rmpc_ctx_set_cold_start(RmpcCtx *c, int32_t mode) {
+    if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
+    if (mode != 0 && mode != 1) return fail(RMPC_EINVAL, "cold-start mode %d: 0 or 1", mode);
+    c->cold_rows = mode == 1;
+    for (auto &sc : c->sub) sc->cold_rows = mode == 1;
     return RMPC_OK;
 }
 
@@ -630,6 +639,7 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
                      : fast_cap > 0           ? fast_cap
                      : c->fast_cap > 0        ? c->fast_cap
                                               : (p->horizon <= 20 ? (lti ? 9 : 7) : 12);
+        a.init_zc = c->cold_rows ? 1 : 0;  // rmpc_ctx_set_cold_start
         // the tail continues from each handed-on robot's sets (retry_sets)
         HIP_TRY(c->retry_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
         a.retry_sets = (uint32_t *)c->retry_sets.p;

@@ -451,6 +451,43 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
             Bf.set(j, v);
         }
     }
+    else if (a.init_zc) {
+        // Zero-correction start: the hinge rows the reference inputs alone would violate start
+        // active (the free response x_{k+1} = A_k x_k (+ c_k), du = 0).  The QP and its optimum
+        // are unchanged; only the first PDAS iterate is closer to it.
+        T x0 = d0, x1 = d1, x2 = d2;
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            if (k > 0) {
+                const T px = PX(k), py = PY(k);
+                uint32_t h = 0;
+#pragma unroll
+                for (int o = 0; o < (NO > 0 ? NOL : RMPC_MAX_OBSTACLES); o++) {
+                    if (NO == 0 && o >= a.no) break;
+                    const T ox = obs_s[3 * (obase + o)], oy = obs_s[3 * (obase + o) + 1], sf = obs_s[3 * (obase + o) + 2];
+                    const T ddx = px - ox, ddy = py - oy;
+                    const T dd = ddx * ddx + ddy * ddy;
+                    T y = rsq_approx(dd);
+                    if constexpr (F64) {
+                        const T hh = (T)0.5 * dd * y;
+                        y = fma(y, fma(-hh, y, (T)0.5), y);
+                    }
+                    const T r = fma(-fma(ddy, x1, fma(ddx, x0, dd)), y, sf);
+                    h |= (dd * y > (T)0.01 && r > (T)0) ? (1u << o) : 0u;
+                }
+                Hf.set(k, h);
+            }
+            if constexpr (LTI) {
+                const T n0 = x0 + la0 * x2 + S[k], n1 = x1 + la1 * x2 + Cs[k];
+                x2 = x2 + V0[k];
+                x0 = n0; x1 = n1;
+            } else {
+                const T vr = fabs(V0[k]) > (T)0.01 ? V0[k] : (T)0.1;
+                x0 = x0 + (-vr * S[k] * dt) * x2;
+                x1 = x1 + (vr * Cs[k] * dt) * x2;
+            }
+        }
+    }
     // (fp64 refinement of fp32-certified sets: `extra_cap` more PDAS solves from them)
     const int maxit = a.extra_cap > 0 ? min(p.max_iter, it + a.extra_cap) : maxit0;
     // The last GREG blocks the backward sweep forms (j < GREG) stay in registers instead of the

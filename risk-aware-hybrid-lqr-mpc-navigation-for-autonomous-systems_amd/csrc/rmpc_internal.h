@@ -85,6 +85,7 @@ struct MpcFastArgs {
     uint32_t *prev_sets;
     int prev_shift;
     uint32_t prev_stamp;
+    int init_zc;                     // cold start: hinge rows violated by the free response start active
 };
 // LDS slot.  The LDS-using kernels of the MPC pipeline (the lane-per-robot stage, the lane-group
 // tail, the generic kernel's leftover list) each run one wave per SIMD, four per CU, and with

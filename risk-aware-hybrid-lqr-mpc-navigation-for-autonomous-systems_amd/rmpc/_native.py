@@ -81,6 +81,7 @@ _PROTOS = {
     "rmpc_ctx_set_timing": [_vp, _i32],
     "rmpc_ctx_set_stage_caps": [_vp, _i32, _i32],
     "rmpc_ctx_set_side_stream": [_vp, _i32],
+    "rmpc_ctx_set_cold_start": [_vp, _i32],
     "rmpc_ctx_set_warm_start": [_vp, _i32],
     "rmpc_mpc_stage_times": [_vp, C.POINTER(C.c_double)],
     "rmpc_mpc_solve_batch": [_vp, C.POINTER(MpcParams), _i64, _vp, _vp, _i32, _vp, _i32, _vp, _i32,

@@ -241,6 +241,14 @@ def set_side_stream(on=True, device=0, slot=0):
     check(lib.rmpc_ctx_set_side_stream(nat.context(device, slot), int(bool(on))), "rmpc_ctx_set_side_stream")
 
 
+def set_cold_start(mode=0, device=0, slot=0):
+    """First active sets of a cold solve on one context (rmpc_ctx_set_cold_start): 0 (default)
+    empty, 1 the hinge rows the start error's free response violates.  Same optimum; mode 1
+    pays with batches in flight and costs one batch alone."""
+    lib = nat.load()
+    check(lib.rmpc_ctx_set_cold_start(nat.context(device, slot), int(mode)), "rmpc_ctx_set_cold_start")
+
+
 def set_warm_start(on=True, device=0, slot=0):
     """Warm start across calls on one context (rmpc_ctx_set_warm_start): each whole-batch MPC
     solve starts robot b's active-set iteration from robot b's previous certified sets, shifted

@@ -872,6 +872,39 @@ def test_rollout_used_flag_per_mode(rm):
     assert not rl["used_mpc"].any()
 
 
+def test_cold_start_rows_same_optimum(rm):
+    """rmpc_ctx_set_cold_start(1): PDAS starts from the hinge rows the start error's free response
+    violates instead of empty sets.  The QP is unchanged, so every robot certifies the same
+    optimum (config 3's shape, and config 4's through its fp32 sets and fp64 refinement), with
+    fewer PDAS solves on average."""
+    from rmpc import workloads as W
+    outs = {}
+    try:
+        for mode, slot in ((0, 0), (1, 7)):
+            rm.batch.set_cold_start(mode, slot=slot)
+            res = []
+            for N, obs, prec, seed in ((20, W.DEFAULT_OBS, 0, 11), (30, W.UNION8_OBS, 1, 12)):
+                B = 4096
+                idx = np.arange(B)
+                xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, W.t0_at(idx, B), N + 1)
+                x0 = xr[:, 0] + W.noise_at(idx, seed)
+                p = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02,
+                                          precision=prec)
+                res.append(rm.batch.mpc_solve_batch(p, x0, xr, ur, obs, step_count=np.full(B, 10, np.int32),
+                                                    slot=slot))
+            outs[mode] = res
+    finally:
+        rm.batch.set_cold_start(0, slot=7)
+    for r0, r1 in zip(outs[0], outs[1]):
+        assert np.all(r0["status"] == 0) and np.all(r1["status"] == 0)
+        np.testing.assert_allclose(r1["u_seq"], r0["u_seq"], atol=1e-11, rtol=0)
+        np.testing.assert_allclose(r1["cost"], r0["cost"], rtol=1e-12)
+        np.testing.assert_array_equal(r1["slack_used"], r0["slack_used"])
+    assert outs[1][0]["iters"].mean() < outs[0][0]["iters"].mean()
+    with pytest.raises(rm.RmpcError):
+        rm.batch.set_cold_start(2, slot=7)
+
+
 def _closed_loop_warm_vs_cold(rm, p, B, steps, obs, seed, N, slot=3):
     """One closed loop driven by the cold-started solves (slot 0) while a warm-started context
     (`slot`) solves the same inputs each step; returns per-step outputs of both."""
