@@ -86,6 +86,9 @@ struct RmpcCtx {
     DevBuf fast_gains, retry, retry2, retry_count, prof, retry_sets;
     DevBuf refine, refine_sets;     // fp32 requests: the fp32-certified robots and their sets
     GroupDiag gdiag;           // lane-group tail diagnostics (RMPC_GROUP_CHECK, RMPC_DENSE_PROF=2)
+    // per tail launch site, the list length its last launch saw (host-mapped words the tail
+    // kernel writes; -1 before the first): the next launch's grid (rmpc_launch_mpc_group)
+    int32_t *tail_hint_h = nullptr, *tail_hint_d = nullptr;
     // closed-loop rollout state (rmpc_rollout_batch)
     DevBuf ro_x, ro_xr, ro_ur, ro_u, ro_step, ro_cache, ro_prev, ro_since, ro_status, ro_used,
         ro_risk, ro_counts, ro_off, ro_pred;
@@ -309,6 +312,8 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     c->prof.release();
     c->retry_count.release();
     c->gdiag.release();
+    if (c->tail_hint_h) (void)hipHostFree(c->tail_hint_h);
+    c->tail_hint_h = c->tail_hint_d = nullptr;
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return RMPC_OK;
@@ -549,6 +554,22 @@ size_t rmpc_kernel_static_lds(const void *fn) {
     return v;
 }
 
+// the tail launch site `k`'s hint (RmpcCtx::tail_hint_h): its device word and last length
+enum { TAIL_SITE_MAIN = 0, TAIL_SITE_REFINE = 1, TAIL_SITE_COLD = 2, TAIL_SITES = 8 };
+static hipError_t tail_hint(RmpcCtx *c, int k, int32_t **dev, int *prev) {
+    if (!c->tail_hint_h) {
+        hipError_t e = hipHostMalloc((void **)&c->tail_hint_h, TAIL_SITES * sizeof(int32_t),
+                                     hipHostMallocMapped | hipHostMallocCoherent);
+        if (e != hipSuccess) { c->tail_hint_h = nullptr; return e; }
+        for (int i = 0; i < TAIL_SITES; i++) c->tail_hint_h[i] = -1;
+        e = hipHostGetDevicePointer((void **)&c->tail_hint_d, c->tail_hint_h, 0);
+        if (e != hipSuccess) { (void)hipHostFree(c->tail_hint_h); c->tail_hint_h = nullptr; return e; }
+    }
+    *dev = c->tail_hint_d + k;
+    *prev = __atomic_load_n(c->tail_hint_h + k, __ATOMIC_RELAXED);
+    return hipSuccess;
+}
+
 static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const double *x0,
                       const double *x_refs, int32_t ref_rows, const double *u_refs, int32_t uref_rows,
                       const double *obstacles, int32_t n_obs, int32_t *step_count, double *u0,
@@ -590,10 +611,13 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
         }
         int32_t *cnt2 = cnt + 8;
         const int cap = 11;
+        int32_t *hint_d = nullptr;
+        int hint_p = -1;
+        HIP_TRY(tail_hint(c, TAIL_SITE_COLD, &hint_d, &hint_p));
         HIP_TRY(rmpc_launch_mpc_group(d, p->horizon, lti ? 1 : bs, n_obs, B, x0, x_refs, ref_rows, u_refs,
                                       uref_rows, obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
                                       iters, list, list_n, (int32_t *)c->retry2.p, cnt2, cap, nullptr, s, nullptr,
-                                      lti, &c->gdiag));
+                                      lti, &c->gdiag, nullptr, 0, hint_d, hint_p));
         dbg_sync(s, "group (cold)");
         HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
                                     step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
@@ -712,6 +736,12 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
         // error after the fork joins the side branch first (`join`): the call's stream must
         // never complete ahead of a refinement kernel that is still writing outputs.
         if (group_tail) HIP_TRY(c->retry2.ensure((size_t)B * sizeof(int32_t)));
+        int32_t *hint_d[2] = {nullptr, nullptr};
+        int hint_p[2] = {-1, -1};
+        if (group_tail) {
+            HIP_TRY(tail_hint(c, TAIL_SITE_MAIN, &hint_d[0], &hint_p[0]));
+            HIP_TRY(tail_hint(c, TAIL_SITE_REFINE, &hint_d[1], &hint_p[1]));
+        }
         if (refine_side) {
             HIP_TRY(side_stream(c));
             for (auto &e : c->rev)
@@ -772,7 +802,8 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
             HIP_TRY_J(rmpc_launch_mpc_group(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs, uref_rows,
                                             obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
                                             iters, left, left_n, (int32_t *)c->retry2.p, cnt2, tail_cap,
-                                            a.retry_sets, s, pc, lti, &c->gdiag, a.prev_sets, a.prev_stamp));
+                                            a.retry_sets, s, pc, lti, &c->gdiag, a.prev_sets, a.prev_stamp,
+                                            hint_d[0], hint_p[0]));
             HIP_TRY(join());               // the refinement, before anything else on this stream
 #undef HIP_TRY_J
             if (refine_side) {            // the refinement's hand-ons (same output list)
@@ -780,7 +811,7 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
                                               obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
                                               iters, (const int32_t *)c->retry_r.p, cnt + 10, (int32_t *)c->retry2.p,
                                               cnt2, tail_cap, (const uint32_t *)c->retry_sets_r.p, s, pc, lti,
-                                              &c->gdiag, a.prev_sets, a.prev_stamp));
+                                              &c->gdiag, a.prev_sets, a.prev_stamp, hint_d[1], hint_p[1]));
             }
             if (prof) HIP_TRY(rmpc_diag_print_stage_prof(pc, cnt, refine, s));
             dbg_sync(s, "group");

@@ -48,6 +48,8 @@ struct GroupArgs {
     uint32_t *prev_sets;              // warm start across calls (MpcFastArgs::prev_sets): per robot,
                                       // [N + NB + 1][nB]; a certified robot's sets are written back
     uint32_t prev_stamp;              // ... with this stamp
+    int32_t *count_out;               // optional (host-mapped): the list's length, for the next
+                                      // launch's grid (rmpc_launch_mpc_group)
 };
 
 // RMPC_GROUP_CHECK: an out-of-range index sets a flag bit and (first hit only) records the

@@ -140,7 +140,7 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
                                  int32_t *retry_count, int pdas_cap, const uint32_t *warm,
                                  hipStream_t stream, unsigned long long *prof = nullptr,
                                  bool lti = false, GroupDiag *diag = nullptr, uint32_t *prev_sets = nullptr,
-                                 uint32_t prev_stamp = 0);
+                                 uint32_t prev_stamp = 0, int32_t *count_out = nullptr, int prev_count = -1);
 
 hipError_t rmpc_launch_mpc_f64(const MpcDevParams &prm, const MpcLayout &L, int64_t B,
                                const double *x0, const double *x_refs, int ref_rows,

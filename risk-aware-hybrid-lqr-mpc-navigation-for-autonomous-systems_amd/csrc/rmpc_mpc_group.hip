@@ -50,6 +50,8 @@ __global__ __launch_bounds__(64, 1) void mpc_group_kernel(GroupArgs a) {
     const int rec = GRec<N, NB, T>::size(a.no);
     const int cnt = *a.count;
     if (a.chk && lane == 0 && blockIdx.x == 0 && (cnt < 0 || cnt > a.nB)) diag_hit(a.chk, 2, 4, cnt);
+    if (a.count_out && lane == 0 && blockIdx.x == 0)
+        __hip_atomic_store(a.count_out, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     for (int t0 = blockIdx.x * RPW; t0 < cnt; t0 += gridDim.x * RPW) {
         const int t = t0 + grp;
         group_solve<N, BS, G, T, LTI>(a, lds + grp * rec, t, t < cnt, gl, grp);
@@ -92,7 +94,8 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
                                  const int32_t *index, const int32_t *count, int32_t *retry,
                                  int32_t *retry_count, int pdas_cap, const uint32_t *warm,
                                  hipStream_t stream, unsigned long long *prof, bool lti,
-                                 GroupDiag *diag, uint32_t *prev_sets, uint32_t prev_stamp) {
+                                 GroupDiag *diag, uint32_t *prev_sets, uint32_t prev_stamp,
+                                 int32_t *count_out, int prev_count) {
     if (capacity <= 0) return hipSuccess;
     if (!rmpc_mpc_group_supported(N, bs, no) || (lti && bs != 1)) return hipErrorInvalidValue;
     GroupArgs a;
@@ -112,11 +115,20 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
     a.site = nullptr;
     a.prev_sets = prev_sets;
     a.prev_stamp = prev_stamp;
+    a.count_out = count_out;
     const int G = group_lanes(N, bs), rpw = 64 / G;
     const int64_t need = (capacity + rpw - 1) / rpw;
     // capped grid (the kernel loops over rounds): GROUP_GRID_MAX waves, one per SIMD of the chip
     // (RMPC_GROUP_GRID=<waves>: another cap, A/B)
-    const int64_t gmax = rmpc_knob("RMPC_GROUP_GRID") ? atoll(rmpc_knob("RMPC_GROUP_GRID")) : GROUP_GRID_MAX;
+    int64_t gmax = rmpc_knob("RMPC_GROUP_GRID") ? atoll(rmpc_knob("RMPC_GROUP_GRID")) : GROUP_GRID_MAX;
+    // Sized from the list length this launch site saw last time (prev_count, a host-mapped word
+    // the kernel writes; -1: unknown): every empty workgroup still takes an LDS slot and a SIMD
+    // in flight, where a few hundred of the 1024 have work (config 3, eight batches in flight).
+    // The round loop covers a longer list, so the hint only moves the cost, never the result.
+    if (prev_count >= 0 && !rmpc_knob("RMPC_GROUP_GRID")) {
+        const int64_t want = ((int64_t)prev_count * 3 / 2 + rpw - 1) / rpw + 64;
+        gmax = want < 64 ? 64 : (want < GROUP_GRID_MAX ? want : GROUP_GRID_MAX);
+    }
     const int64_t grid = need < gmax ? need : (gmax > 0 ? gmax : need);
     // diagnostics buffers (RMPC_DENSE_PROF=2, RMPC_GROUP_CHECK): owned by the caller's context
     const char *pe = rmpc_knob("RMPC_DENSE_PROF");

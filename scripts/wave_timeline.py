@@ -10,7 +10,7 @@ batch alone (library default caps, launches back to back), and reports
     what ran before / after each gap;
   - per stage-1 dispatch: span, waves, and when its first / last wave started relative to the
     previous stage-1 dispatch's end.
-Usage: RMPC_DIAG=1 RMPC_LIB_PATH=$PWD/<pkg>/rmpc/librmpc_wlog.so python scripts/wave_timeline.py
+Usage: GPU_MAX_HW_QUEUES=16 RMPC_DIAG=1 RMPC_LIB_PATH=$PWD/<pkg>/rmpc/librmpc_wlog.so python scripts/wave_timeline.py
        [--steps K] [--inflight S] [--caps F,T] [--out gpurun_out/wl.npz]"""
 import argparse
 import ctypes as C
@@ -150,10 +150,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--inflight", type=int, default=3)
+    ap.add_argument("--inflight", type=int, default=8)
     ap.add_argument("--caps", default="9,4")
     ap.add_argument("--out", default="gpurun_out/wl.npz")
     ap.add_argument("--cap-records", type=int, default=1 << 23)
+    ap.add_argument("--cold-start", type=int, default=1, help="in-flight contexts' rmpc_ctx_set_cold_start mode")
     args = ap.parse_args()
     import torch
     import rmpc
@@ -187,6 +188,7 @@ def main():
     for i in range(S):
         rmpc.batch.set_stage_caps(*caps, device=0, slot=i)
         rmpc.batch.set_side_stream(S == 1, device=0, slot=i)
+        rmpc.batch.set_cold_start(args.cold_start if S > 1 else 0, device=0, slot=i)
 
     def step(k):
         i = k % S
@@ -200,6 +202,7 @@ def main():
     for label, nsteps, slots in (("inflight", args.steps, S), ("alone_default_caps", args.steps, 1)):
         if label.startswith("alone"):
             rmpc.batch.set_stage_caps(0, 0, device=0, slot=0)
+            rmpc.batch.set_cold_start(0, device=0, slot=0)
             rmpc.batch.set_side_stream(True, device=0, slot=0)
         run = (lambda k: step(k)) if slots > 1 else (lambda k: step(0))
         for k in range(max(args.warmup, S)):
