@@ -22,6 +22,10 @@ for _p in (ROOT, PKG_DIR):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
+# Version of the JSON line's field meanings.  3 (round 4 on): value_one_batch_alone and
+# roofline.kernel_avg_ms are the library-default-caps launch; the in-flight-caps launch moved to
+# value_one_batch_alone_inflight_caps (before round 4 value_one_batch_alone was that launch).
+SCHEMA = 3
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector (= FP64 matrix) dense peak, SURVEY.md 8(d)
 FP32_PEAK_TFLOPS = 157.3    # MI355X FP32 vector dense peak (MI355X_MICROARCH.md chip table)
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
@@ -541,6 +545,7 @@ def main():
         # launch), and with the in-flight stage caps
         "value_one_batch_alone": B_total / alone_default_s,
         "value_one_batch_alone_inflight_caps": B_total / k_avg_s,
+        "schema": SCHEMA,
         "unit": "solves/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -1017,6 +1022,7 @@ def bench_other(args, world, rank, local, dist, pre=None):
     line = {"metric": metric, "value": B_total * args.steps / elapsed,
             "value_one_batch_alone": B_total / (alone_default_s or k_avg_s), "unit": unit, "n_gpus": world,
             **({"value_one_batch_alone_inflight_caps": B_total / k_avg_s} if alone_default_s else {}),
+            "schema": SCHEMA,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: Figure-8 references at per-robot time offsets + seeded start noise",
