@@ -345,11 +345,18 @@ def main():
                     help="FAST,TAIL: the in-flight contexts' stage caps instead of the tuned ones (sweeps)")
     ap.add_argument("--presort", type=int, default=0,
                     help="A/B: order each fleet's robots by predicted difficulty within blocks of this size")
+    ap.add_argument("--alone-side", type=int, default=None, choices=[0, 1],
+                    help="config 5's one-batch-alone measurement: the context's side stream on (1, the "
+                         "library default) or off (0).  Default: off when --hw-queues raised the queue "
+                         "count (with 16 queues mapped, the side stream's fork/join per step costs more "
+                         "than it overlaps: 108M against 146M steps/s; on HIP's default 4 queues the "
+                         "side stream gives 171M)")
     ap.add_argument("--inflight-side", action="store_true",
                     help="keep the library's side streams on the in-flight contexts (A/B; default off there)")
-    ap.add_argument("--inflight", type=int, default=8,
-                    help="MPC configs: batches in flight at once, each on its own stream with its own "
-                         "solver context and outputs (step k runs on stream k mod S)")
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="batches in flight at once, each on its own stream with its own solver "
+                         "context and outputs (step k runs on stream k mod S); default 8, config 2 3 "
+                         "(its ~7 us LQR launches are host-bound: 758M controls/s at 3 against 380M at 8)")
     ap.add_argument("--cold-start", type=int, default=1, choices=[0, 1],
                     help="in-flight contexts' first active sets (rmpc_ctx_set_cold_start): 1 zero-correction rows")
     ap.add_argument("--hw-queues", type=int, default=16,
@@ -367,6 +374,10 @@ def main():
     ap.add_argument("--selftest-fail-rank", type=int, default=-1,
                     help="--selftest: this rank exits with status 3 after joining the group (launcher test)")
     args = ap.parse_args()
+    if args.inflight is None:
+        args.inflight = 3 if args.config == "cfg2" else 8
+    if args.alone_side is None:
+        args.alone_side = 0 if args.hw_queues > 4 else 1
     # (before anything initialises HIP: the setting is read once per process; spawned ranks
     # inherit it)
     if args.hw_queues > 0:
@@ -1014,7 +1025,9 @@ def bench_other(args, world, rank, local, dist, pre=None):
         torch.cuda.synchronize()
         rmpc.batch.set_stage_caps(0, 0, device=local, slot=0)
         rmpc.batch.set_cold_start(0, device=local, slot=0)
+        rmpc.batch.set_side_stream(bool(args.alone_side), device=local, slot=0)
         alone_default_s = alone_times(lambda: step(0), torch.cuda.current_stream(), args.steps)[0] / 1e3
+        rmpc.batch.set_side_stream(True, device=local, slot=0)
         rmpc.batch.set_stage_caps(*caps, device=local, slot=0)
         rmpc.batch.set_cold_start(args.cold_start if S > 1 else 0, device=local, slot=0)
     k_roof_s = alone_default_s or k_avg_s     # the roofline's launch: one batch alone, library defaults
@@ -1030,6 +1043,7 @@ def bench_other(args, world, rank, local, dist, pre=None):
                        "parallelism": parallelism(args, world), "batches_in_flight": S}}
     if args.config == "cfg5":
         line["config"]["stage_caps"] = list(caps) if caps[0] else "library default"
+        line["config"]["alone_side_stream"] = bool(args.alone_side)
     if flops_unit:
         ach = flops_unit * B / k_roof_s / 1e12
         line["roofline"] = {"bound": "valu-fp64", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -125,9 +125,13 @@ hipError_t rmpc_launch_mpc_group(const MpcDevParams &prm, int N, int bs, int no,
     // the kernel writes; -1: unknown): every empty workgroup still takes an LDS slot and a SIMD
     // in flight, where a few hundred of the 1024 have work (config 3, eight batches in flight).
     // The round loop covers a longer list, so the hint only moves the cost, never the result.
+    // A list longer than GROUP_GRID_MAX rounds (the LTI-group path's whole batches) keeps a
+    // workgroup per round: looping 16 rounds per workgroup left the launch waiting on the
+    // workgroups whose rounds held the hardest robots (LTI one batch alone 169M -> 157M).
     if (prev_count >= 0 && !rmpc_knob("RMPC_GROUP_GRID")) {
-        const int64_t want = ((int64_t)prev_count * 3 / 2 + rpw - 1) / rpw + 64;
-        gmax = want < 64 ? 64 : (want < GROUP_GRID_MAX ? want : GROUP_GRID_MAX);
+        const int64_t rounds = ((int64_t)prev_count + rpw - 1) / rpw;
+        const int64_t want = rounds > GROUP_GRID_MAX ? rounds + 64 : rounds * 3 / 2 + 64;
+        gmax = rounds > GROUP_GRID_MAX ? want : (want < GROUP_GRID_MAX ? want : GROUP_GRID_MAX);
     }
     const int64_t grid = need < gmax ? need : (gmax > 0 ? gmax : need);
     // diagnostics buffers (RMPC_DENSE_PROF=2, RMPC_GROUP_CHECK): owned by the caller's context
