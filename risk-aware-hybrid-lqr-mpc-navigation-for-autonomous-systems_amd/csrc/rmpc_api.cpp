@@ -89,6 +89,7 @@ struct RmpcCtx {
     // per tail launch site, the list length its last launch saw (host-mapped words the tail
     // kernel writes; -1 before the first): the next launch's grid (rmpc_launch_mpc_group)
     int32_t *tail_hint_h = nullptr, *tail_hint_d = nullptr;
+    int32_t tail_est[8] = {-1, -1, -1, -1, -1, -1, -1, -1};   // per site: decaying max of the lengths seen
     // closed-loop rollout state (rmpc_rollout_batch)
     DevBuf ro_x, ro_xr, ro_ur, ro_u, ro_step, ro_cache, ro_prev, ro_since, ro_status, ro_used,
         ro_risk, ro_counts, ro_off, ro_pred;
@@ -566,7 +567,17 @@ static hipError_t tail_hint(RmpcCtx *c, int k, int32_t **dev, int *prev) {
         if (e != hipSuccess) { (void)hipHostFree(c->tail_hint_h); c->tail_hint_h = nullptr; return e; }
     }
     *dev = c->tail_hint_d + k;
-    *prev = __atomic_load_n(c->tail_hint_h + k, __ATOMIC_RELAXED);
+    const int32_t v = __atomic_load_n(c->tail_hint_h + k, __ATOMIC_RELAXED);
+#if RMPC_HINT_LAST
+    *prev = v;
+#else
+    // a decaying maximum (1/8 per launch) of the lengths the launches at this site wrote: a
+    // list that fluctuates from call to call (closed loops) keeps the grid of its longer calls,
+    // where the last length alone left rounds of two on the critical path
+    int32_t &e = c->tail_est[k];
+    if (v >= 0) e = e < 0 ? v : (v > e - e / 8 ? v : e - e / 8);
+    *prev = e;
+#endif
     return hipSuccess;
 }
 
