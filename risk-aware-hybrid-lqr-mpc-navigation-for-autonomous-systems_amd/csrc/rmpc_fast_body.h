@@ -320,21 +320,28 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
                 const int64_t bq = a.index ? (int64_t)a.index[tq] : tq;
                 row[q] = a.prm.ref_off ? (int64_t)a.prm.ref_off[bq] : bq;
             }
-            auto stage = [&](const double *src, const int W, const int rows, const int ne, auto put)
+            // both arrays' loads are issued before the first LDS round (RMPC_SETUP_PF; 0: each
+            // array's loads right before its own rounds, two memory latencies per wave); not for
+            // paired lanes, whose fp64 N = 30 instance then spills (38 VGPRs against 2)
+#ifndef RMPC_SETUP_PF
+#define RMPC_SETUP_PF 1
+#endif
+            auto ld = [&](const double *src, const int W, const int rows, const int ne, auto &v)
                 __attribute__((always_inline)) {
-                constexpr int NP = (3 * N + 15) / 16;        // rounds (sized for x_refs; u_refs uses fewer)
-                double v[NP][RW / 4];
+                constexpr int NP = sizeof(v) / sizeof(v[0]);
 #pragma unroll
                 for (int ps = 0; ps < NP; ps++)
 #pragma unroll
                     for (int q = 0; q < RW / 4; q++) {
                         const int e = 16 * ps + ee;
                         const int64_t r0 = a.prm.ref_off ? row[q] : row[q] * rows;   // (ref_row0)
-                        v[ps][q] = (16 * ps < ne && e < ne) ? src[r0 * W + e] : 0.0;
+                        v[ps][q] = e < ne ? src[r0 * W + e] : 0.0;
                     }
+            };
+            auto rounds = [&](const int ne, auto &v, auto put) __attribute__((always_inline)) {
+                constexpr int NP = sizeof(v) / sizeof(v[0]);
 #pragma unroll
                 for (int ps = 0; ps < NP; ps++) {
-                    if (16 * ps >= ne) break;
                     __syncthreads();
 #pragma unroll
                     for (int q = 0; q < RW / 4; q++) stg[(4 * q + rr) * SP + ee] = v[ps][q];
@@ -344,16 +351,23 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
                         if (16 * ps + i < ne) put(16 * ps + i, stg[ll * SP + i]);
                 }
             };
-            stage(a.x_refs, 3, a.ref_rows, 3 * N, [&](const int e, const double v) __attribute__((always_inline)) {
+            auto putx = [&](const int e, const double v) __attribute__((always_inline)) {
                 if (e % 3 == 0) PX(e / 3) = (T)v;
                 else if (e % 3 == 1) PY(e / 3) = (T)v;
                 else if constexpr (F64) S[e / 3] = v;        // the heading, for the loop below
                 else TH[e / 3] = v;
-            });
-            stage(a.u_refs, 2, a.uref_rows, 2 * N, [&](const int e, const double v) __attribute__((always_inline)) {
+            };
+            auto putu = [&](const int e, const double v) __attribute__((always_inline)) {
                 if (e % 2 == 0) V0[e / 2] = (T)v;
                 else V1(e / 2) = (T)v;
-            });
+            };
+            double vx[(3 * N + 15) / 16][RW / 4], vu[(2 * N + 15) / 16][RW / 4];
+            ld(a.x_refs, 3, a.ref_rows, 3 * N, vx);
+            constexpr bool SPF = RMPC_SETUP_PF && PR == 1;
+            if constexpr (SPF) ld(a.u_refs, 2, a.uref_rows, 2 * N, vu);
+            rounds(3 * N, vx, putx);
+            if constexpr (!SPF) ld(a.u_refs, 2, a.uref_rows, 2 * N, vu);
+            rounds(2 * N, vu, putu);
         }
 #pragma unroll
         for (int k = 0; k < N; k++) {
