@@ -408,3 +408,43 @@ def test_mpc_repeated_calls_reuse_zeroed_list_counters(rm):
     for k in small:
         np.testing.assert_array_equal(small[k], fresh[k], err_msg=k)
         np.testing.assert_array_equal(small[k], runs[0][k][:1000], err_msg=k)
+
+
+def test_mpc_tail_grid_sizes_give_the_same_bits(rm):
+    """The tail kernel's grid is sized from the list lengths its launch site saw before (a
+    decaying maximum, rmpc_api.cpp tail_hint; a list longer than the 1024-round cap gets a
+    workgroup per round, rmpc_mpc_group.hip) and its workgroups loop over rounds of robots, so
+    the grid must not change any result.  Config 3's full batch after a 64-robot solve on the
+    same fresh context (a 64-workgroup grid for ~900 rounds: ~14 rounds per workgroup) against
+    the full batch on another fresh context (1024 workgroups); and LTI's full batch twice on a
+    third context (the capped grid, then a workgroup per round): bit for bit."""
+    import torch
+    x0h, xrh, urh = cfg3_inputs()
+    dev = torch.device("cuda:0")
+    x0, xr, ur = (torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (x0h, xrh, urh))
+    obs = torch.tensor(ompc.default_obstacles(), dtype=torch.float64, device=dev).reshape(-1, 3)
+    B = x0.shape[0]
+
+    def solve(p, slot, n=B):
+        o = dict(u0=torch.empty(n, 2, dtype=torch.float64, device=dev),
+                 u_seq=torch.empty(n, N, 2, dtype=torch.float64, device=dev),
+                 x_pred=torch.empty(n, N + 1, 3, dtype=torch.float64, device=dev),
+                 status=torch.empty(n, dtype=torch.int32, device=dev),
+                 iters=torch.empty(n, dtype=torch.int32, device=dev))
+        rm.batch.mpc_solve_batch_dev(p, x0[:n], xr[:n], ur[:n], obs, o,
+                                     step_count=torch.full((n,), 10, dtype=torch.int32, device=dev), slot=slot)
+        torch.cuda.synchronize()
+        return {k: v.cpu().numpy() for k, v in o.items()}
+
+    ltv = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+    solve(ltv, 11, 64)
+    small_grid = solve(ltv, 11)
+    fresh = solve(ltv, 12)
+    assert np.all(fresh["status"] == 0) and (fresh["iters"] > 7).sum() > 1000   # a long tail list
+    for k in fresh:
+        np.testing.assert_array_equal(small_grid[k], fresh[k], err_msg=k)
+    lti = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02, ltv=False)
+    first, second = solve(lti, 13), solve(lti, 13)
+    assert np.all(first["status"] == 0)
+    for k in first:
+        np.testing.assert_array_equal(first[k], second[k], err_msg=k)
