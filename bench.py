@@ -458,10 +458,13 @@ def main():
     # with batches in flight the chip's idle time is filled by the other batches, and a longer
     # lane-per-robot stage (less work for the lane-group tail) pays (scripts/r02_s3_caps*.sh,
     # three in flight): config 3 (9, 4) against the single-batch default (7, 4), LTI (13, 4)
-    # against (9, 4), config 4 (14, 6) against (12, 6)
+    # against (9, 4), config 4 (14, 6) against (12, 6); round 5, eight in flight with the
+    # zero-correction first sets: config 3's tail cap 3 before projected Newton (9, 3) against
+    # (9, 4) at the driver's 20 steps, six pairs: +3% mean, 100 steps +0.6%
+    # (profiles/r05/session_46.txt, session_47.txt)
     caps = (0, 0)
     if S > 1:
-        caps = (14, 6) if N > 20 else ((13, 4) if args.lti else (9, 4))
+        caps = (14, 6) if N > 20 else ((13, 4) if args.lti else (9, 3))
     if args.stage_caps:
         caps = tuple(int(v) for v in args.stage_caps.split(","))
     for i in range(S):
