@@ -245,40 +245,58 @@ def timed_loop(step, steps, warmup, dist, sync, S=1):
     return time.perf_counter() - t0
 
 
-def gather_loop(step, local_u0, dist, world, rank, steps, sync, cdev):
-    """N > 1: K more steps with SURVEY 8(e)'s batch gather inside the timed region -- after
-    every step the rank's u0 shard is all-gathered and interleaved back into global robot order
-    (rmpc.workloads.gather_interleaved; RCCL over xGMI, or gloo through the host).  Returns
-    (slowest rank's elapsed s, the last gathered u0 [world * B, 2] on cdev)."""
+def gather_loop(step, local_u0, dist, world, rank, steps, sync, cdev, S=1, stream_of=None):
+    """N > 1: K more steps with SURVEY 8(e)'s batch gather inside the timed region, in the same
+    pipeline as the timed loop: step k runs on in-flight slot i = k mod S, and right after its
+    solve, slot i's u0 shard is all-gathered and interleaved back into global robot order
+    (rmpc.workloads.gather_interleaved) on slot i's own stream (`stream_of(i)`), into a buffer
+    of that slot's own -- so the collective waits only for its own batch and the other slots'
+    batches stay in flight (RCCL over xGMI; gloo through the host).  Returns (slowest rank's
+    elapsed s, the last gathered u0 [world * B, 2] of every slot on cdev, the slots visited)."""
+    import contextlib
+    import torch
     from rmpc import workloads as W
-    g_out = None
+    bufs, last, visited = [None] * S, [None] * S, set()
 
-    def step_gather():
-        nonlocal g_out
-        step()
-        g, g_out = W.gather_interleaved(dist, local_u0().to(cdev), world, g_out)
-        return g
-    step_gather()
+    def step_gather(k):
+        i = k % S
+        step(k)
+        with (torch.cuda.stream(stream_of(i)) if stream_of else contextlib.nullcontext()):
+            last[i], bufs[i] = W.gather_interleaved(dist, local_u0(i).to(cdev), world, bufs[i])
+        visited.add(i)
+    for k in range(S):
+        step_gather(k)
     sync()
     dist.barrier()
     sync()
     t = time.perf_counter()
-    for _ in range(steps):
-        g = step_gather()
+    for k in range(steps):
+        step_gather(k)
     sync()
     dist.barrier()
     elapsed = time.perf_counter() - t
-    assert bool((g[rank::world] == local_u0().to(cdev)).all())
+    for i in range(S):
+        assert bool((last[i][rank::world] == local_u0(i).to(cdev)).all()), i
     elapsed, _ = W.aggregate(dist, elapsed, [], device=cdev)
-    return elapsed, g
+    return elapsed, last, sorted(visited)
+
+
+def gather_label(dist, B, S):
+    """What `value_with_gather` measures, named after the backend actually used."""
+    be = dist.get_backend()
+    coll = "RCCL all_gather over xGMI" if be == "nccl" else f"{be} all_gather through the host"
+    return (f"{coll} of u0 ({B} x 2 fp64 per rank) after every step, on that step's in-flight slot's stream "
+            f"(S = {S} slots, rotated as in the timed loop), inside the timed region")
 
 
 def selftest_rank(args, world, rank):
     """--selftest: one rank of the multi-rank flow on the CPU (gloo), with the oracle's C port
     standing in for the device solve (a checker of the launcher and collectives, never a
-    measurement): its round-robin shard of a config-3 batch, the setup broadcast, the timed
-    loop, the gathered leg and the MAX / SUM aggregation -- the same functions as the GPU run.
-    Rank 0 prints one JSON line (and saves the gathered u0 with --selftest-out)."""
+    measurement): its round-robin shard of S config-3 fleets (--inflight S, bench.py's fleets),
+    the setup broadcast, the timed loop over the slots, the gathered leg (every slot's u0
+    gathered after its step) and the MAX / SUM aggregation -- the same functions as the GPU run.
+    Rank 0 prints one JSON line (and saves the gathered u0 of every slot, [S, W * B, 2], with
+    --selftest-out)."""
     import numpy as np
     import torch
     from oracle import cpu, figure8
@@ -288,36 +306,45 @@ def selftest_rank(args, world, rank):
     if rank == args.selftest_fail_rank:
         sys.exit(3)                        # the others now block in their first collective
     cfg = W.CONFIGS["cfg3"]
+    S = max(1, args.inflight) if args.inflight_given else 1
     N, B_total = cfg["N"], args.selftest_batch * world
     idx = W.shard_indices(B_total, world, rank)
-    xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, W.t0_at(idx, B_total), N + 1)
-    x0 = xr[:, 0] + W.noise_at(idx, cfg["seed"])
+    fleets = []
+    for f in range(S):
+        xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, W.fleet_t0(idx, B_total, f, S), N + 1)
+        fleets.append((xr[:, 0] + W.noise_at(idx, W.fleet_seed(cfg["seed"], f)), xr, ur))
     obs = torch.tensor(cfg["obs"], dtype=torch.float64) if rank == 0 else torch.zeros(len(cfg["obs"]), 3, dtype=torch.float64)
     obs = W.broadcast_shared(dist, obs)
     p = cpu.mpc_params(N, (15, 15, 50), (.1, .1), (30, 30, 40), 0.3, 5000., 2., 3., 0.02)
-    res = {}
+    res = [None] * S
 
     def step(k=0):
-        res["out"] = cpu.mpc_solve_batch(p, x0, xr, ur, obs.numpy(), step_count=np.full(idx.size, 10, np.int32))
+        x0, xr, ur = fleets[k % S]
+        res[k % S] = cpu.mpc_solve_batch(p, x0, xr, ur, obs.numpy(), step_count=np.full(idx.size, 10, np.int32))
     nosync = lambda: None                                      # noqa: E731
-    elapsed = timed_loop(step, args.steps, args.warmup, dist, nosync)
-    u0 = lambda: torch.from_numpy(res["out"]["u0"])            # noqa: E731
-    elapsed_g, g = (None, u0()) if dist is None else gather_loop(step, u0, dist, world, rank, args.steps,
-                                                                 nosync, torch.device("cpu"))
-    st = res["out"]["status"]
+    elapsed = timed_loop(step, args.steps, args.warmup, dist, nosync, S)
+    u0 = lambda i: torch.from_numpy(res[i]["u0"])              # noqa: E731
+    visited = [0]
+    if dist is None:
+        elapsed_g, g = None, [u0(i) for i in range(S)]
+    else:
+        elapsed_g, g, visited = gather_loop(step, u0, dist, world, rank, args.steps, nosync, torch.device("cpu"), S)
+    st = np.concatenate([r["status"] for r in res])
     elapsed, counts = W.aggregate(dist, elapsed, [int((st == c).sum()) for c in (0, 1, 2)])
     line = {"metric": "SELFTEST (C port on the CPU, not a measurement): MPC QP solves/sec", "selftest": True,
             "value": B_total * args.steps / elapsed, "unit": "solves/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"cfg3 shape, {args.selftest_batch} robots/rank", "global_batch": B_total,
-                       "parallelism": f"batch-split x{world}, gloo"},
+                       "parallelism": f"batch-split x{world}, gloo", "batches_in_flight": S},
             "solver": dict(optimal=counts[0], inaccurate=counts[1], fallback=counts[2])}
     if elapsed_g is not None:
         line["value_with_gather"] = B_total * args.steps / elapsed_g
+        line["gather"] = gather_label(dist, idx.size, S)
+        line["gather_slots_visited"] = visited
     if rank == 0:
         if args.selftest_out:
-            np.save(args.selftest_out, g.numpy())
+            np.save(args.selftest_out, torch.stack(g).numpy())
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
@@ -343,6 +370,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline work budget")
     ap.add_argument("--stage-caps", default=None,
                     help="FAST,TAIL: the in-flight contexts' stage caps instead of the tuned ones (sweeps)")
+    ap.add_argument("--stage-passes", default=None,
+                    help="C1[,C2]: the in-flight contexts' stage-1 passes (rmpc_ctx_set_stage_passes) "
+                         "instead of the tuned ones; 0 = one pass")
     ap.add_argument("--presort", type=int, default=0,
                     help="A/B: order each fleet's robots by predicted difficulty within blocks of this size")
     ap.add_argument("--alone-side", type=int, default=None, choices=[0, 1],
@@ -374,6 +404,7 @@ def main():
     ap.add_argument("--selftest-fail-rank", type=int, default=-1,
                     help="--selftest: this rank exits with status 3 after joining the group (launcher test)")
     args = ap.parse_args()
+    args.inflight_given = args.inflight is not None
     if args.inflight is None:
         args.inflight = 3 if args.config == "cfg2" else 8
     if args.alone_side is None:
@@ -456,26 +487,20 @@ def main():
     alone_default_s = None
     streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(S - 1)]
     # with batches in flight the chip's idle time is filled by the other batches, and a longer
-    # lane-per-robot stage (less work for the lane-group tail) pays (scripts/r02_s3_caps*.sh,
-    # three in flight): config 3 (9, 4) against the single-batch default (7, 4), LTI (13, 4)
-    # against (9, 4), config 4 (14, 6) against (12, 6); round 5, eight in flight with the
-    # zero-correction first sets: config 3's tail cap 3 before projected Newton (9, 3) against
-    # (9, 4) at the driver's 20 steps, six pairs: +3% mean, 100 steps +0.6%
-    # (profiles/r05/session_46.txt, session_47.txt)
-    caps = (0, 0)
-    if S > 1:
-        caps = (14, 6) if N > 20 else ((13, 4) if args.lti else (9, 3))
+    # lane-per-robot stage (less work for the lane-group tail) pays; the zero-correction first
+    # sets lower the total PDAS work; side streams would add to the streams sharing the
+    # hardware queues (rmpc.workloads.INFLIGHT: the settings, and where each was measured)
+    st = W.inflight_settings(args.config, args.lti) if S > 1 else dict(W.ALONE)
     if args.stage_caps:
-        caps = tuple(int(v) for v in args.stage_caps.split(","))
+        st["caps"] = tuple(int(v) for v in args.stage_caps.split(","))
+    if args.stage_passes:
+        st["passes"] = tuple(int(v) for v in (args.stage_passes + ",0").split(",")[:2])
+    if S > 1:
+        st["cold_start"] = args.cold_start
+        st["side"] = args.inflight_side
+    caps = st["caps"]
     for i in range(S):
-        rmpc.batch.set_stage_caps(*caps, device=local, slot=i)
-        # in flight, the other batches overlap each other, and the side streams would add to the
-        # streams sharing the hardware queues: off there (rmpc_ctx_set_side_stream; config 4
-        # 69.9M against 66.0M solves/s, profiles/r03/ab_side_streams_in_flight.txt)
-        rmpc.batch.set_side_stream(S == 1 or args.inflight_side, device=local, slot=i)
-        # in flight the total PDAS work sets the rate, not the hardest robot's chain: the
-        # zero-correction first sets (rmpc_ctx_set_cold_start)
-        rmpc.batch.set_cold_start(args.cold_start if S > 1 else 0, device=local, slot=i)
+        rmpc.batch.configure(st, device=local, slot=i)
 
     def step(k=0):
         i = k % S
@@ -492,12 +517,12 @@ def main():
     k_avg_s = k_ms / 1e3
     # ... and with the library's default stage caps on a context of its own (what one batch at
     # a time would use; its side stream on, rmpc_ctx_set_side_stream)
-    if caps[0]:
-        rmpc.batch.set_stage_caps(0, 0, device=local, slot=S)
+    if S > 1:
+        rmpc.batch.configure(W.ALONE, device=local, slot=S)
         alone_default_s = alone_times(lambda: rmpc.batch.mpc_solve_batch_dev(
             p, x0, xr, ur, obs, outs[0], step_count=counts_sc[0], device=local, stream=stream, slot=S),
             stream, args.steps)[0] / 1e3
-    if alone_default_s is None or not caps[0]:
+    if alone_default_s is None:
         alone_default_s = k_avg_s
 
     # the roofline prices one batch alone at the library's defaults: the launch the rocprofv3
@@ -505,8 +530,7 @@ def main():
     k_roof_s = alone_default_s
     # per-stage device time of that launch (separate, untimed pass: events between the
     # pipeline's kernels; only the lane-per-robot pipeline has stages)
-    rmpc.batch.set_stage_caps(0, 0, device=local, slot=0)
-    rmpc.batch.set_cold_start(0, device=local, slot=0)
+    rmpc.batch.configure(dict(W.ALONE, side=st["side"]), device=local, slot=0)
     rmpc.batch.set_stage_timing(True, device=local)
     stage = []
     try:
@@ -517,16 +541,15 @@ def main():
     except rmpc.RmpcError:
         stage_ms = None
     rmpc.batch.set_stage_timing(False, device=local)
-    rmpc.batch.set_stage_caps(*caps, device=local, slot=0)
-    rmpc.batch.set_cold_start(args.cold_start if S > 1 else 0, device=local, slot=0)
+    rmpc.batch.configure(st, device=local, slot=0)
 
     # N > 1: the same K steps again with the batch gather of u0 inside the timed region
     # (SURVEY 8(e)'s collective: RCCL all_gather over xGMI; the round-robin shards interleave
     # back into global robot order by a transpose of the [world][B] result)
     elapsed_g = None
     if dist:
-        elapsed_g, u0_global = gather_loop(step, lambda: out["u0"], dist, world, rank, args.steps,
-                                           torch.cuda.synchronize, cdev)
+        elapsed_g, _, gather_slots = gather_loop(step, lambda i: outs[i]["u0"], dist, world, rank, args.steps,
+                                                 torch.cuda.synchronize, cdev, S, lambda i: streams[i])
 
     st = out["status"].cpu().numpy()
     its = out["iters"].cpu().numpy()
@@ -575,7 +598,9 @@ def main():
                                f"Q=[15,15,50] R=[.1,.1] P=[30,30,40] rho=5000, {B_per} robots/GPU",
                    "robots_per_gpu": B_per, "global_batch": B_total, "horizon": N,
                    "n_obstacles": n_obs, "parallelism": parallelism(args, world),
-                   "batches_in_flight": S, "stage_caps": list(caps) if caps[0] else "library default"},
+                   "batches_in_flight": S, "stage_caps": list(caps) if caps[0] else "library default",
+                   "stage_passes": list(st["passes"]) if st["passes"][0] else "one pass",
+                   "zero_correction_first_sets": bool(st["cold_start"])},
         # compute-bound path on the vector ALU (MFMA unused by the default pipeline): priced at
         # the FP64 (FP32 for config 4) vector peak.  `achieved`/`frac` use SURVEY 8(d)'s
         # canonical condensed-QP flop count; `frac_executed` is what the kernels actually
@@ -605,8 +630,8 @@ def main():
     }
     if elapsed_g is not None:
         line["value_with_gather"] = B_total * args.steps / elapsed_g
-        line["gather"] = (f"RCCL all_gather of u0 ({B} x 2 fp64 per rank) after every step, "
-                          "inside the timed region")
+        line["gather"] = gather_label(dist, B, S)
+        line["gather_slots_visited"] = gather_slots
 
     # ---- PCIe-inclusive rate (rank 0, N=1 only; never `value`): the host-pointer C-ABI
     # (rmpc_mpc_solve_batch) with pageable numpy buffers, staged H2D/D2H by the library
@@ -1002,14 +1027,17 @@ def bench_other(args, world, rank, local, dist, pre=None):
 
         # in flight, the MPC branch's first stage runs longer (scripts/r02_s3_caps_cfg.sh:
         # fast cap 9 against the single-batch default 6)
-        caps = (9, 4) if S > 1 else (0, 0)
+        # (config 5 keeps its side stream in flight: 398-418M against 233M steps/s without)
+        st = W.inflight_settings("cfg5") if S > 1 else dict(W.ALONE)
         if args.stage_caps:
-            caps = tuple(int(v) for v in args.stage_caps.split(","))
+            st["caps"] = tuple(int(v) for v in args.stage_caps.split(","))
+        if args.stage_passes:
+            st["passes"] = tuple(int(v) for v in (args.stage_passes + ",0").split(",")[:2])
+        if S > 1:
+            st["cold_start"] = args.cold_start
+        caps = st["caps"]
         for i in range(S):
-            rmpc.batch.set_stage_caps(*caps, device=local, slot=i)
-            # (config 5 keeps its side stream in flight: 398-418M against 233M steps/s without)
-            rmpc.batch.set_side_stream(True, device=local, slot=i)
-            rmpc.batch.set_cold_start(args.cold_start if S > 1 else 0, device=local, slot=i)
+            rmpc.batch.configure(st, device=local, slot=i)
 
         def step(k=0):
             i = k % S
@@ -1026,13 +1054,9 @@ def bench_other(args, world, rank, local, dist, pre=None):
     if args.config == "cfg5" and caps[0]:
         # one batch alone with the library's default caps (what one batch at a time would use)
         torch.cuda.synchronize()
-        rmpc.batch.set_stage_caps(0, 0, device=local, slot=0)
-        rmpc.batch.set_cold_start(0, device=local, slot=0)
-        rmpc.batch.set_side_stream(bool(args.alone_side), device=local, slot=0)
+        rmpc.batch.configure(dict(W.ALONE, side=bool(args.alone_side)), device=local, slot=0)
         alone_default_s = alone_times(lambda: step(0), torch.cuda.current_stream(), args.steps)[0] / 1e3
-        rmpc.batch.set_side_stream(True, device=local, slot=0)
-        rmpc.batch.set_stage_caps(*caps, device=local, slot=0)
-        rmpc.batch.set_cold_start(args.cold_start if S > 1 else 0, device=local, slot=0)
+        rmpc.batch.configure(st, device=local, slot=0)
     k_roof_s = alone_default_s or k_avg_s     # the roofline's launch: one batch alone, library defaults
     elapsed, _ = W.aggregate(dist, elapsed, [], device=coll_device(args, dev))
     line = {"metric": metric, "value": B_total * args.steps / elapsed,

@@ -157,6 +157,15 @@ int rmpc_ctx_set_timing(RmpcCtx *ctx, int32_t on);
  * (HISTORY.md section 1: (9, 4) at BASELINE configs 3 and 5).  They apply to the hybrid
  * step's MPC branch too (its default first-stage cap is 6).  fast_cap, tail_cap in [0, 64]. */
 int rmpc_ctx_set_stage_caps(RmpcCtx *ctx, int32_t fast_cap, int32_t tail_cap);
+/* Passes of the lane-per-robot stage on this context (a performance setting; results are the
+ * same QP optimum, and the same iterate path robot by robot): with first_cap > 0 the stage runs
+ * every robot for first_cap PDAS solves, then continues only the uncertified robots, compacted
+ * into dense waves from their active sets and iteration counts, up to second_cap solves (0: no
+ * third pass) and then up to the stage cap.  A pass whose cap is not below the stage cap is
+ * skipped.  0, 0 (the default): one pass.  With batches in flight the compaction recovers the
+ * lane slots that certified robots leave idle in a one-pass wave (HISTORY.md section 11).
+ * Caps in [0, 64], second_cap above first_cap or 0. */
+int rmpc_ctx_set_stage_passes(RmpcCtx *ctx, int32_t first_cap, int32_t second_cap);
 /* Side stream on this context (a performance setting; results are identical): on (default),
  * a pipeline's independent branch -- the fp64 refinement of an fp32 request beside the tail,
  * the hybrid step's LQR branch beside the MPC branch -- runs on a second stream of the context,

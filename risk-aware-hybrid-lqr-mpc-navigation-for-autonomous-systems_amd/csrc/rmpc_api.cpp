@@ -85,6 +85,9 @@ struct RmpcCtx {
     DevBuf idx_lqr, idx_mpc, counts, hyb_status;
     DevBuf fast_gains, retry, retry2, retry_count, prof, retry_sets;
     DevBuf refine, refine_sets;     // fp32 requests: the fp32-certified robots and their sets
+    // multi-pass lane-per-robot stage: the earlier passes' hand-on lists and their sets
+    DevBuf pass_list[2], pass_sets[2];
+    int passes[2] = {0, 0};           // rmpc_ctx_set_stage_passes: the earlier passes' caps (0: none)
     GroupDiag gdiag;           // lane-group tail diagnostics (RMPC_GROUP_CHECK, RMPC_DENSE_PROF=2)
     // per tail launch site, the list length its last launch saw (host-mapped words the tail
     // kernel writes; -1 before the first): the next launch's grid (rmpc_launch_mpc_group)
@@ -302,6 +305,7 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     if (c->last_ev) (void)hipEventDestroy(c->last_ev);
     c->retry_r.release();
     c->retry_sets_r.release();
+    for (int i = 0; i < 2; i++) { c->pass_list[i].release(); c->pass_sets[i].release(); }
     c->retry2.release();
     c->retry_sets.release();
     c->refine.release();
@@ -352,6 +356,20 @@ int rmpc_ctx_set_stage_caps(RmpcCtx *c, int32_t fast_cap, int32_t tail_cap) {
     for (auto &sc : c->sub) {
         sc->fast_cap = fast_cap;
         sc->tail_cap = tail_cap;
+    }
+    return RMPC_OK;
+}
+
+int rmpc_ctx_set_stage_passes(RmpcCtx *c, int32_t first_cap, int32_t second_cap) {
+    if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
+    if (first_cap < 0 || first_cap > 64 || second_cap < 0 || second_cap > 64 ||
+        (second_cap > 0 && second_cap <= first_cap))
+        return fail(RMPC_EINVAL, "pass caps must be in [0, 64], the second above the first (or 0)");
+    c->passes[0] = first_cap;
+    c->passes[1] = first_cap > 0 ? second_cap : 0;
+    for (auto &sc : c->sub) {
+        sc->passes[0] = c->passes[0];
+        sc->passes[1] = c->passes[1];
     }
     return RMPC_OK;
 }
@@ -556,7 +574,8 @@ size_t rmpc_kernel_static_lds(const void *fn) {
 }
 
 // the tail launch site `k`'s hint (RmpcCtx::tail_hint_h): its device word and last length
-enum { TAIL_SITE_MAIN = 0, TAIL_SITE_REFINE = 1, TAIL_SITE_COLD = 2, TAIL_SITES = 8 };
+enum { TAIL_SITE_MAIN = 0, TAIL_SITE_REFINE = 1, TAIL_SITE_COLD = 2, TAIL_SITE_GENERIC = 3,
+       TAIL_SITE_GENERIC_COLD = 4, TAIL_SITES = 8 };
 static hipError_t tail_hint(RmpcCtx *c, int k, int32_t **dev, int *prev) {
     if (!c->tail_hint_h) {
         hipError_t e = hipHostMalloc((void **)&c->tail_hint_h, TAIL_SITES * sizeof(int32_t),
@@ -630,10 +649,13 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
                                       iters, list, list_n, (int32_t *)c->retry2.p, cnt2, cap, nullptr, s, nullptr,
                                       lti, &c->gdiag, nullptr, 0, hint_d, hint_p));
         dbg_sync(s, "group (cold)");
+        int32_t *ghint_d = nullptr;
+        int ghint_p = -1;
+        HIP_TRY(tail_hint(c, TAIL_SITE_GENERIC_COLD, &ghint_d, &ghint_p));
         HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
                                     step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
                                     c->ws.p, (const int32_t *)c->retry2.p, cnt2, s, rmpc_mpc_lds_lanes(L),
-                                    other_counts(c)));
+                                    other_counts(c), ghint_d, ghint_p));
         if (B > 0) flip_counts(c);
         return RMPC_OK;
     }
@@ -736,6 +758,38 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
             a.refine_sets = (uint32_t *)c->refine_sets.p;
         }
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[0], s));
+        // Multi-pass stage: pass i runs its robots for up to caps[i] PDAS solves in total and
+        // hands the uncertified ones on, with their sets and iteration counts, to a compacted
+        // list; the next pass continues exactly there (MpcFastArgs::warm_sets), so the iterate
+        // path is the one-pass path and only the packing of robots into waves changes: a later
+        // pass's waves hold no robot that has already certified.  The last pass runs to the
+        // stage cap and hands on to the tail.
+        int caps[2], ncap = 0;
+        for (int i = 0; i < 2; i++)
+            if (c->passes[i] > (ncap ? caps[ncap - 1] : 0) && c->passes[i] < a.pdas_cap) caps[ncap++] = c->passes[i];
+        if (const char *sp = rmpc_knob("RMPC_FAST_SPLIT")) {   // (A/B: "c1[,c2]", "0" = one pass)
+            ncap = 0;
+            for (const char *q = sp; *q && ncap < 2;) {
+                const int v = atoi(q);
+                if (v > (ncap ? caps[ncap - 1] : 0) && v < a.pdas_cap) caps[ncap++] = v;
+                while (*q && *q != ',') q++;
+                if (*q == ',') q++;
+            }
+        }
+        for (int i = 0; i < ncap; i++) {
+            HIP_TRY(c->pass_list[i].ensure((size_t)B * sizeof(int32_t)));
+            HIP_TRY(c->pass_sets[i].ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
+            MpcFastArgs ai = a;
+            ai.pdas_cap = caps[i];
+            ai.retry = (int32_t *)c->pass_list[i].p;
+            ai.retry_count = cnt + 2 + i;
+            ai.retry_sets = (uint32_t *)c->pass_sets[i].p;
+            HIP_TRY(rmpc_launch_mpc_fast(ai, p->horizon, bs, prec, s, lti));
+            dbg_sync(s, "fast pass");
+            a.index = ai.retry;            // the next pass: that list, from its sets
+            a.count = ai.retry_count;
+            a.warm_sets = ai.retry_sets;
+        }
         HIP_TRY(rmpc_launch_mpc_fast(a, p->horizon, bs, prec, s, lti));
         // tail: the lane-group Riccati kernel (RMPC_DISABLE_DENSE: no tail stage, A/B only)
         const bool group_tail = rmpc_mpc_group_supported(p->horizon, bs, n_obs) && !rmpc_knob("RMPC_DISABLE_DENSE");
@@ -833,9 +887,13 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
         // what remains is rare (cycling beyond both, non-finite data): LDS generic kernel, in
         // the requested arithmetic (the lane-group tail between is fp64 for both)
         // (a refined fp32 request stays fp64 here too: every output it returns is the fp64 optimum)
+        int32_t *ghint_d = nullptr;
+        int ghint_p = -1;
+        HIP_TRY(tail_hint(c, TAIL_SITE_GENERIC, &ghint_d, &ghint_p));
         HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
                                         step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
-                                        c->ws.p, left, left_n, s, rmpc_mpc_lds_lanes(L), other_counts(c)));
+                                        c->ws.p, left, left_n, s, rmpc_mpc_lds_lanes(L), other_counts(c),
+                                        ghint_d, ghint_p));
         if (B > 0) flip_counts(c);         // (the next pipeline takes the set zeroed there)
         if (c->timing) {
             HIP_TRY(hipEventRecord(c->ev[3], s));

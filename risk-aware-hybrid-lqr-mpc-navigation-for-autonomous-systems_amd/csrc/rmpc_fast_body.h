@@ -189,7 +189,7 @@ template <> struct Big<float> { static constexpr float v = 1e30f; };
 // is built both ways and the cold one launched when prev_sets is null: the read and write-back
 // cost its register allocation ~1% (profiles/r03/ab_warm_start.txt).
 template <int N, int BS, typename T, bool LTI, int NO = 0, int PR = 1, bool WS = true>
-__device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
+__device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid, int &its_out) {
     static_assert(!LTI || BS == 1, "LTI ignores move blocking");
     static_assert(PR == 1 || (PR == 2 && NO > 0 && NO % 2 == 0 && BS == 1 && !LTI && NO / 2 <= 4),
                   "paired lanes: compile-time rows, split evenly, block size 1, LTV");
@@ -502,6 +502,7 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
             }
         }
     }
+    const int it_start = it;
     // (fp64 refinement of fp32-certified sets: `extra_cap` more PDAS solves from them)
     const int maxit = a.extra_cap > 0 ? min(p.max_iter, it + a.extra_cap) : maxit0;
     // The last GREG blocks the backward sweep forms (j < GREG) stay in registers instead of the
@@ -976,6 +977,7 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid) {
         if (sig == hist0 || sig == hist1 || sig == hist2 || sig == hist3) break;
         hist3 = hist2; hist2 = hist1; hist1 = hist0; hist0 = sig;
     }
+    its_out = it - it_start;
     if (a.prof) {      // wave totals = max over lanes (the last lane saw every iteration)
         unsigned long long mb = tp_b, mf = tp_f, mi = (unsigned long long)it;
         for (int off = 32; off > 0; off >>= 1) {

@@ -149,7 +149,7 @@ hipError_t rmpc_launch_mpc_f64(const MpcDevParams &prm, const MpcLayout &L, int6
                                double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
                                int32_t *iters, void *ws, const int32_t *index,
                                const int32_t *count, hipStream_t stream, int lds_lanes = 0,
-                               int32_t *zero_next = nullptr);
+                               int32_t *zero_next = nullptr, int32_t *count_out = nullptr, int prev_count = -1);
 hipError_t rmpc_launch_mpc_f32(const MpcDevParams &prm, const MpcLayout &L, int64_t B,
                                const double *x0, const double *x_refs, int ref_rows,
                                const double *u_refs, int uref_rows, const double *obstacles,
@@ -157,7 +157,7 @@ hipError_t rmpc_launch_mpc_f32(const MpcDevParams &prm, const MpcLayout &L, int6
                                double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
                                int32_t *iters, void *ws, const int32_t *index,
                                const int32_t *count, hipStream_t stream, int lds_lanes = 0,
-                               int32_t *zero_next = nullptr);
+                               int32_t *zero_next = nullptr, int32_t *count_out = nullptr, int prev_count = -1);
 // lanes per workgroup for the LDS-resident generic kernel (0 = record too large for LDS)
 int rmpc_mpc_lds_lanes(const MpcLayout &L);
 

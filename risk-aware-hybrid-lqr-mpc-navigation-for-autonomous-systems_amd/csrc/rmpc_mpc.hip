@@ -40,6 +40,9 @@ struct MpcArgs {
     // the calling context's other list-counter set (RMPC_COUNT_WORDS words), zeroed by
     // workgroup 0 for the context's next call, which takes it (may be null)
     int32_t *zero_next;
+    // leftover-list launches: the list length this launch saw, written to a host-mapped word
+    // (the next launch's grid; may be null)
+    int32_t *count_out;
 };
 
 // ------------------------------------------------------------------------------ setup
@@ -620,10 +623,12 @@ __device__ __forceinline__ void mpc_solve_one(const MpcArgs<T> &a, int64_t t) {
     if (a.iters) a.iters[b] = it;
 }
 
-#define GENERIC_GRID_MAX 16
-// USE_LDS (the small retry lists after the tails): a grid of GENERIC_GRID_MAX workgroups
-// looping over the list, so an empty or short list does not dispatch capacity / lanes
-// workgroups that each hold 128 KB of LDS only to exit
+#define GENERIC_GRID_MIN 16
+// USE_LDS (the leftover lists after the tails): a grid sized from the list lengths this launch
+// site saw before, at least GENERIC_GRID_MIN workgroups, looping over the list -- an empty or
+// short list (the usual few robots) does not dispatch capacity / lanes workgroups that each
+// hold an LDS slot only to exit, and a long one (non-finite inputs, many cycling robots) is not
+// left to a few workgroups
 template <typename T, bool USE_LDS>
 __global__ __launch_bounds__(256) void mpc_solve_kernel(MpcArgs<T> a) {
     RMPC_WLOG_BEGIN
@@ -631,6 +636,7 @@ __global__ __launch_bounds__(256) void mpc_solve_kernel(MpcArgs<T> a) {
     const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (a.zero_next && t0 == 0)
         for (int i = 0; i < RMPC_COUNT_WORDS; i++) a.zero_next[i] = 0;
+    if (a.count_out && t0 == 0) __hip_atomic_store(a.count_out, (int32_t)nrob, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if constexpr (USE_LDS) {
         for (int64_t t = t0; t < nrob; t += (int64_t)gridDim.x * blockDim.x) mpc_solve_one<T, true>(a, t);
     } else {
@@ -690,7 +696,8 @@ static hipError_t launch_generic(const MpcDevParams &prm, const MpcLayout &L, in
                                int n_obs, int32_t *step_count, double *u0, double *u_seq,
                                double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
                                int32_t *iters, void *ws, const int32_t *index,
-                               const int32_t *count, hipStream_t stream, int lds_lanes, int32_t *zero_next) {
+                               const int32_t *count, hipStream_t stream, int lds_lanes, int32_t *zero_next,
+                               int32_t *count_out, int prev_count) {
     MpcArgs<T> a;
     a.prm = prm;
     a.L = L;
@@ -704,6 +711,7 @@ static hipError_t launch_generic(const MpcDevParams &prm, const MpcLayout &L, in
     a.index = index;
     a.count = count;
     a.zero_next = zero_next;
+    a.count_out = index ? count_out : nullptr;
     if (B <= 0) return hipSuccess;
     if (lds_lanes > 0) {
         const size_t lds = rmpc_lds_slot_pad((const void *)mpc_solve_kernel<T, true>, (size_t)L.REC * lds_lanes * sizeof(T));
@@ -725,12 +733,20 @@ static hipError_t launch_generic(const MpcDevParams &prm, const MpcLayout &L, in
             if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
             n_cu.store(v);
         }
-        // a few workgroups looping over the (short) list: each one has to find a free LDS slot
-        // in flight (RMPC_GENERIC_GRID=<workgroups>: another cap, A/B)
-        int64_t blocks = (B + lds_lanes - 1) / lds_lanes, cap = GENERIC_GRID_MAX;
+        // workgroups looping over the list, each of which has to find a free LDS slot in flight:
+        // 1.5x the rounds of the longest recent list (prev_count: a decaying maximum of the
+        // lengths this site's launches wrote; -1 unknown), at least GENERIC_GRID_MIN, at most
+        // four per CU (RMPC_GENERIC_GRID=<workgroups>: a fixed cap, A/B).  A short guess costs
+        // rounds, never results.
+        int64_t blocks = (B + lds_lanes - 1) / lds_lanes, cap = GENERIC_GRID_MIN;
+        if (prev_count > 0) {
+            const int64_t rounds = ((int64_t)prev_count + lds_lanes - 1) / lds_lanes;
+            const int64_t want = rounds + rounds / 2;
+            cap = want > cap ? want : cap;
+        }
+        if (cap > 4 * (int64_t)n_cu.load()) cap = 4 * (int64_t)n_cu.load();
         if (const char *g = rmpc_knob("RMPC_GENERIC_GRID")) cap = atoll(g) > 0 ? atoll(g) : cap;
         if (blocks > cap) blocks = cap;
-        if (blocks > n_cu.load()) blocks = n_cu.load();
         hipLaunchKernelGGL((mpc_solve_kernel<T, true>), dim3((unsigned)blocks), dim3(lds_lanes), lds,
                            stream, a);
     } else {
@@ -748,10 +764,11 @@ hipError_t rmpc_launch_mpc_f64(const MpcDevParams &prm, const MpcLayout &L, int6
                                int n_obs, int32_t *step_count, double *u0, double *u_seq,
                                double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
                                int32_t *iters, void *ws, const int32_t *index,
-                               const int32_t *count, hipStream_t stream, int lds_lanes, int32_t *zero_next) {
+                               const int32_t *count, hipStream_t stream, int lds_lanes, int32_t *zero_next,
+                               int32_t *count_out, int prev_count) {
     return launch_generic<double>(prm, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
                                   step_count, u0, u_seq, x_pred, cost, status, slack_used, iters, ws, index,
-                                  count, stream, lds_lanes, zero_next);
+                                  count, stream, lds_lanes, zero_next, count_out, prev_count);
 }
 
 // fp32 arithmetic (BASELINE config 4): same algorithm, float workspace; inputs/outputs stay fp64
@@ -761,8 +778,9 @@ hipError_t rmpc_launch_mpc_f32(const MpcDevParams &prm, const MpcLayout &L, int6
                                int n_obs, int32_t *step_count, double *u0, double *u_seq,
                                double *x_pred, double *cost, int32_t *status, uint8_t *slack_used,
                                int32_t *iters, void *ws, const int32_t *index,
-                               const int32_t *count, hipStream_t stream, int lds_lanes, int32_t *zero_next) {
+                               const int32_t *count, hipStream_t stream, int lds_lanes, int32_t *zero_next,
+                               int32_t *count_out, int prev_count) {
     return launch_generic<float>(prm, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
                                  step_count, u0, u_seq, x_pred, cost, status, slack_used, iters, ws, index,
-                                 count, stream, lds_lanes, zero_next);
+                                 count, stream, lds_lanes, zero_next, count_out, prev_count);
 }

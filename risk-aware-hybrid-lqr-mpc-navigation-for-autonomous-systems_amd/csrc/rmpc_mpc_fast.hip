@@ -24,8 +24,9 @@ namespace rmpc {
 template <int N, int BS, typename T, bool LTI, int NO = 0, int PR = 1, bool WS = true>
 __global__ __launch_bounds__(64, 1) void mpc_ltv_fast_kernel(MpcFastArgs a) {
     RMPC_WLOG_BEGIN
-    fast_body<N, BS, T, LTI, NO, PR, WS>(a, blockIdx.x);
-    RMPC_WLOG_END(WL_FAST)
+    int wl_its = 0;     // (wave-log builds: this lane's PDAS iterations in the launch)
+    fast_body<N, BS, T, LTI, NO, PR, WS>(a, blockIdx.x, wl_its);
+    RMPC_WLOG_END_ITS(WL_FAST, wl_its)
 }
 }  // namespace rmpc
 RMPC_WLOG_SETTER(rmpc_wlog_set_fast)

@@ -41,8 +41,15 @@ __device__ __forceinline__ unsigned wl_take() {
     return i < g_wlog.cap / 64u ? sh * (g_wlog.cap / 64u) + i : ~0u;
 }
 
-// at the wave's end (every lane calls; lane 0 writes)
-__device__ __forceinline__ void wl_record(int kid, unsigned slot, unsigned long long t0) {
+// at the wave's end (every lane calls; lane 0 writes).  `its`: this lane's PDAS iterations in
+// the launch (stage 1; 0 elsewhere): the record keeps the wave's maximum and the lanes' sum
+// (lane utilisation = sum / (64 x max))
+__device__ __forceinline__ void wl_record(int kid, unsigned slot, unsigned long long t0, int its = 0) {
+    int mx = its, sm = its;
+    for (int off = 32; off > 0; off >>= 1) {
+        mx = max(mx, __shfl_xor(mx, off));
+        sm += __shfl_xor(sm, off);
+    }
     if (threadIdx.x != 0 || slot == ~0u) return;
 #if RMPC_WLOG_DRAIN
     // (variant: the end after the wave's outstanding memory operations -- its last stores --
@@ -54,7 +61,8 @@ __device__ __forceinline__ void wl_record(int kid, unsigned slot, unsigned long 
     const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
     const unsigned long long dp = (unsigned long long)__builtin_amdgcn_dispatch_ptr();
     unsigned long long *r = g_wlog.rec + 4ull * slot;
-    r[0] = ((unsigned long long)kid << 32) | blockIdx.x;
+    r[0] = ((unsigned long long)kid << 56) | ((unsigned long long)(mx & 0xff) << 48) |
+           ((unsigned long long)(sm & 0xffff) << 32) | blockIdx.x;
     r[1] = t0;
     r[2] = t1;
     r[3] = (((dp >> 6) & 0xffffffull) << 40) | ((unsigned long long)(xcc & 0xff) << 32) | hw;
@@ -64,10 +72,12 @@ __device__ __forceinline__ void wl_record(int kid, unsigned slot, unsigned long 
     const unsigned long long wl_t0_ = __builtin_amdgcn_s_memrealtime(); \
     const unsigned wl_slot_ = rmpc::wl_take();
 #define RMPC_WLOG_END(kid) rmpc::wl_record(kid, wl_slot_, wl_t0_);
+#define RMPC_WLOG_END_ITS(kid, its) rmpc::wl_record(kid, wl_slot_, wl_t0_, its);
 #define RMPC_WLOG_SETTER(name) \
     extern "C" hipError_t name(rmpc::WaveLog w) { return hipMemcpyToSymbol(HIP_SYMBOL(rmpc::g_wlog), &w, sizeof w); }
 #else
 #define RMPC_WLOG_BEGIN
 #define RMPC_WLOG_END(kid)
+#define RMPC_WLOG_END_ITS(kid, its)
 #define RMPC_WLOG_SETTER(name)
 #endif

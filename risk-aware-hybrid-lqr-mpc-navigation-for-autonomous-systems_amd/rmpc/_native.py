@@ -80,6 +80,7 @@ _PROTOS = {
     "rmpc_device_count": [C.POINTER(C.c_int)],
     "rmpc_ctx_set_timing": [_vp, _i32],
     "rmpc_ctx_set_stage_caps": [_vp, _i32, _i32],
+    "rmpc_ctx_set_stage_passes": [_vp, _i32, _i32],
     "rmpc_ctx_set_side_stream": [_vp, _i32],
     "rmpc_ctx_set_cold_start": [_vp, _i32],
     "rmpc_ctx_set_warm_start": [_vp, _i32],
@@ -209,6 +210,15 @@ def release_context(h):
         _lib.rmpc_ctx_destroy(h)
 
 
+def _release_quietly(h):
+    """Finalizer form of release_context: at interpreter exit the library or the HIP runtime
+    may already be torn down, and a destroy that fails there has nothing left to release."""
+    try:
+        release_context(h)
+    except Exception:
+        pass
+
+
 class OwnedContext:
     """One caller's own context (own_context), destroyed exactly once: by release(), or by a
     weakref finalizer when the owner is collected (also at interpreter exit, before the
@@ -217,7 +227,7 @@ class OwnedContext:
 
     def __init__(self, device=0):
         self.h = own_context(device)
-        self._fin = weakref.finalize(self, release_context, self.h)
+        self._fin = weakref.finalize(self, _release_quietly, self.h)
 
     def release(self):
         self._fin()

@@ -234,6 +234,24 @@ def set_stage_caps(fast_cap=0, tail_cap=0, device=0, slot=0):
           "rmpc_ctx_set_stage_caps")
 
 
+def set_stage_passes(first_cap=0, second_cap=0, device=0, slot=0):
+    """Passes of the lane-per-robot stage on one context (rmpc_ctx_set_stage_passes): the first
+    pass runs every robot for `first_cap` PDAS solves, the next ones continue only the
+    uncertified robots in compacted waves.  Same optimum and iterate path; (0, 0) = one pass."""
+    lib = nat.load()
+    check(lib.rmpc_ctx_set_stage_passes(nat.context(device, slot), int(first_cap), int(second_cap)),
+          "rmpc_ctx_set_stage_passes")
+
+
+def configure(settings, device=0, slot=0):
+    """All performance settings of one context at once: `settings` a dict with caps (fast,
+    tail), cold_start, passes (first, second) and side (rmpc.workloads.INFLIGHT / ALONE)."""
+    set_stage_caps(*settings["caps"], device=device, slot=slot)
+    set_cold_start(settings["cold_start"], device=device, slot=slot)
+    set_stage_passes(*settings["passes"], device=device, slot=slot)
+    set_side_stream(settings["side"], device=device, slot=slot)
+
+
 def set_side_stream(on=True, device=0, slot=0):
     """Side stream of one context (rmpc_ctx_set_side_stream): the refinement of fp32 requests
     and the hybrid step's LQR branch beside the main branch (on, the default) or in order."""

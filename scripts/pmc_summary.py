@@ -18,4 +18,4 @@ for k, d in tot.items():
     print(k)
     for c, v in sorted(d.items()):
         n = len(calls[k][c])
-        print(f"   {c:28s} per-dispatch {v / max(n, 1):16.4g}   (dispatches {n})")
+        print(f"   {c:28s} per-dispatch {v / max(n, 1):16.4g}   (dispatches {n}, total {v:.4g})")

@@ -29,7 +29,9 @@ KNAME = {1: "fast", 2: "group", 3: "solve"}
 
 
 def decode(rec):
-    kid = (rec[:, 0] >> 32).astype(np.int64)
+    kid = (rec[:, 0] >> 56).astype(np.int64)
+    wits = ((rec[:, 0] >> 48) & 0xff).astype(np.int64)     # stage 1: the wave's PDAS iterations
+    lits = ((rec[:, 0] >> 32) & 0xffff).astype(np.int64)   # ... and its lanes' sum
     blk = (rec[:, 0] & 0xffffffff).astype(np.int64)
     t0, t1 = rec[:, 1].astype(np.int64), rec[:, 2].astype(np.int64)
     hw = (rec[:, 3] & 0xffffffff).astype(np.int64)
@@ -37,7 +39,7 @@ def decode(rec):
     disp = (rec[:, 3] >> 40).astype(np.int64)      # dispatch packet address bits (reused by the ring)
     # gfx9 HW_ID: simd [5:4], cu [11:8], sh [12], se [15:13]
     simd_key = (xcc << 16) | (hw & 0xff30)
-    return dict(kid=kid, blk=blk, t0=t0, t1=t1, simd=simd_key, disp=disp)
+    return dict(kid=kid, blk=blk, t0=t0, t1=t1, simd=simd_key, disp=disp, wits=wits, lits=lits)
 
 
 def dispatches(d, kid):
@@ -77,6 +79,12 @@ def analyse(d, us_per_tick, label):
         rep[name] = {"waves": int(m.sum()), "simd_us": float(x.sum()),
                      "simd_frac": float(x.sum() / (simds.size * win)),
                      "dur_us_p10_50_90_max": [round(float(np.percentile(x, q)), 2) for q in (10, 50, 90)] + [round(float(x.max()), 2)]}
+        if name == "fast":
+            # lane utilisation of the PDAS loop: lane-iterations / (64 x wave-iterations)
+            wi, li = d["wits"][m].sum(), d["lits"][m].sum()
+            rep[name]["wave_iterations"] = int(wi)
+            rep[name]["lane_iterations"] = int(li)
+            rep[name]["lane_utilisation"] = float(li / max(1, 64 * wi))
         if name == "group":
             short = x < 2.0
             rep[name]["empty_waves(<2us)"] = int(short.sum())

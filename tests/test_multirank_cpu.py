@@ -179,34 +179,43 @@ def _bench(args, env=None, timeout=240):
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("world,per_rank", [(2, 512), (8, 256)])
-def test_bench_launcher_spawns_ranks_and_gathers(tmp_path, world, per_rank):
+@pytest.mark.parametrize("world,per_rank,S", [(2, 512, 1), (8, 256, 1), (2, 256, 3)])
+def test_bench_launcher_spawns_ranks_and_gathers(tmp_path, world, per_rank, S):
     """`python bench.py --gpus N` with no launcher starts its own N ranks (bench.spawn_ranks:
     child processes with RANK / WORLD_SIZE / MASTER_*), here through the CPU self-test mode
     (gloo, the C port in place of the device solve; the same timing loop, aggregate and
     gather_interleaved as the GPU run).  Exactly one JSON line comes back, with n_gpus N and the
     gathered leg; the gathered u0 is bit-identical to one process solving the whole batch.
     N = 8 is the driver's scaling node (BASELINE config 4): the launcher, the
-    timing collectives and the 8-way interleaved gather run at the real rank count."""
+    timing collectives and the 8-way interleaved gather run at the real rank count.
+    S = 3: three fleets in flight (--inflight 3, bench.py's slots): the gathered leg rotates the
+    slots like the timed loop, visits every one, and each slot's gathered u0 equals one process
+    solving that fleet."""
     import json
     from oracle import cpu, figure8
     out = tmp_path / "u0.npy"
-    r = _bench(["--gpus", str(world), "--selftest", "--selftest-batch", str(per_rank), "--steps", "2",
-                "--warmup", "1", "--selftest-out", str(out)], timeout=360)
+    r = _bench(["--gpus", str(world), "--selftest", "--selftest-batch", str(per_rank), "--steps", str(max(2, S)),
+                "--warmup", "1", "--selftest-out", str(out)] + (["--inflight", str(S)] if S > 1 else []),
+               timeout=360)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
     assert line["n_gpus"] == world and line["selftest"] is True
     assert line["value"] > 0 and line["value_with_gather"] > 0
+    assert line["gather_slots_visited"] == list(range(S))
+    assert line["gather"].startswith("gloo all_gather")
     B_total, N = world * per_rank, 20
-    assert line["config"]["global_batch"] == B_total and line["solver"]["optimal"] == B_total
+    assert line["config"]["global_batch"] == B_total and line["solver"]["optimal"] == B_total * S
+    g = np.load(out)
+    assert g.shape == (S, B_total, 2)
     idx = np.arange(B_total)
-    xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, W.t0_at(idx, B_total), N + 1)
-    x0 = xr[:, 0] + W.noise_at(idx, W.CONFIGS["cfg3"]["seed"])
     p = cpu.mpc_params(N, (15, 15, 50), (.1, .1), (30, 30, 40), 0.3, 5000., 2., 3., 0.02)
-    ref = cpu.mpc_solve_batch(p, x0, xr, ur, W.DEFAULT_OBS, step_count=np.full(B_total, 10, np.int32))
-    np.testing.assert_array_equal(np.load(out), ref["u0"])
+    for f in range(S):
+        xr, ur = figure8.offset_segments(2.0, 0.5, 0.02, W.fleet_t0(idx, B_total, f, S), N + 1)
+        x0 = xr[:, 0] + W.noise_at(idx, W.fleet_seed(W.CONFIGS["cfg3"]["seed"], f))
+        ref = cpu.mpc_solve_batch(p, x0, xr, ur, W.DEFAULT_OBS, step_count=np.full(B_total, 10, np.int32))
+        np.testing.assert_array_equal(g[f], ref["u0"])
 
 
 @pytest.mark.timeout(300)
