@@ -448,3 +448,38 @@ def test_mpc_tail_grid_sizes_give_the_same_bits(rm):
     assert np.all(first["status"] == 0)
     for k in first:
         np.testing.assert_array_equal(first[k], second[k], err_msg=k)
+
+
+def test_tail_multi_round_loop_bounds_checked(rm, monkeypatch, capfd):
+    """The lane-group tail loops its workgroups over rounds of robots on a grid sized from the
+    list lengths its launch site saw (round 1's persistent form of this loop faulted; HISTORY.md
+    section 10).  With the bounds-check instrumentation on (RMPC_GROUP_CHECK=2: every robot
+    index, list count, retry slot and list entry checked, each wave's last site recorded in
+    host-mapped memory), the multi-round shapes: config 3's full batch after a 64-robot solve
+    on the same fresh context (a small grid, ~14 rounds per workgroup), and LTI's full batch
+    twice (the whole batch through the tail: capped grid, then a workgroup per round).  No check
+    fires, every wave reaches the kernel's exit (site 8), and every robot is optimal."""
+    import re
+    monkeypatch.setenv("RMPC_DIAG", "1")
+    monkeypatch.setenv("RMPC_GROUP_CHECK", "2")
+    x0, xr, ur = cfg3_inputs()
+    obs = ompc.default_obstacles()
+    ltv = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+    lti = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02, ltv=False)
+    capfd.readouterr()
+    outs = [rm.batch.mpc_solve_batch(ltv, x0[:64], xr[:64], ur[:64], obs, device=0, slot=14),
+            rm.batch.mpc_solve_batch(ltv, x0, xr, ur, obs, device=0, slot=14),
+            rm.batch.mpc_solve_batch(lti, x0, xr, ur, obs, device=0, slot=15),
+            rm.batch.mpc_solve_batch(lti, x0, xr, ur, obs, device=0, slot=15)]
+    err = capfd.readouterr().err
+    checks = re.findall(r"\[group check\] grid (\d+): flags (-?\d+)", err)
+    sites = re.findall(r"waves by last site 0\.\.9:((?: \d+)+)", err)
+    assert len(checks) >= 4 and len(sites) == len(checks), err[-2000:]
+    grids = [int(g) for g, _ in checks]
+    assert all(int(f) == 0 for _, f in checks), checks
+    for g, h in zip(grids, sites):
+        hist = [int(v) for v in h.split()]
+        assert hist[8] == g and sum(hist) == g, (g, hist)
+    assert grids[1] < 128            # config 3's ~900 tail rounds on the 64-robot call's small grid
+    for o in outs:
+        assert np.all(o["status"] == 0)
