@@ -490,17 +490,17 @@ def main():
     # lane-per-robot stage (less work for the lane-group tail) pays; the zero-correction first
     # sets lower the total PDAS work; side streams would add to the streams sharing the
     # hardware queues (rmpc.workloads.INFLIGHT: the settings, and where each was measured)
-    st = W.inflight_settings(args.config, args.lti) if S > 1 else dict(W.ALONE)
+    cset = W.inflight_settings(args.config, args.lti) if S > 1 else dict(W.ALONE)
     if args.stage_caps:
-        st["caps"] = tuple(int(v) for v in args.stage_caps.split(","))
+        cset["caps"] = tuple(int(v) for v in args.stage_caps.split(","))
     if args.stage_passes:
-        st["passes"] = tuple(int(v) for v in (args.stage_passes + ",0").split(",")[:2])
+        cset["passes"] = tuple(int(v) for v in (args.stage_passes + ",0").split(",")[:2])
     if S > 1:
-        st["cold_start"] = args.cold_start
-        st["side"] = args.inflight_side
-    caps = st["caps"]
+        cset["cold_start"] = args.cold_start
+        cset["side"] = args.inflight_side
+    caps = cset["caps"]
     for i in range(S):
-        rmpc.batch.configure(st, device=local, slot=i)
+        rmpc.batch.configure(cset, device=local, slot=i)
 
     def step(k=0):
         i = k % S
@@ -530,7 +530,7 @@ def main():
     k_roof_s = alone_default_s
     # per-stage device time of that launch (separate, untimed pass: events between the
     # pipeline's kernels; only the lane-per-robot pipeline has stages)
-    rmpc.batch.configure(dict(W.ALONE, side=st["side"]), device=local, slot=0)
+    rmpc.batch.configure(dict(W.ALONE, side=cset["side"]), device=local, slot=0)
     rmpc.batch.set_stage_timing(True, device=local)
     stage = []
     try:
@@ -541,7 +541,7 @@ def main():
     except rmpc.RmpcError:
         stage_ms = None
     rmpc.batch.set_stage_timing(False, device=local)
-    rmpc.batch.configure(st, device=local, slot=0)
+    rmpc.batch.configure(cset, device=local, slot=0)
 
     # N > 1: the same K steps again with the batch gather of u0 inside the timed region
     # (SURVEY 8(e)'s collective: RCCL all_gather over xGMI; the round-robin shards interleave
@@ -599,8 +599,8 @@ def main():
                    "robots_per_gpu": B_per, "global_batch": B_total, "horizon": N,
                    "n_obstacles": n_obs, "parallelism": parallelism(args, world),
                    "batches_in_flight": S, "stage_caps": list(caps) if caps[0] else "library default",
-                   "stage_passes": list(st["passes"]) if st["passes"][0] else "one pass",
-                   "zero_correction_first_sets": bool(st["cold_start"])},
+                   "stage_passes": list(cset["passes"]) if cset["passes"][0] else "one pass",
+                   "zero_correction_first_sets": bool(cset["cold_start"])},
         # compute-bound path on the vector ALU (MFMA unused by the default pipeline): priced at
         # the FP64 (FP32 for config 4) vector peak.  `achieved`/`frac` use SURVEY 8(d)'s
         # canonical condensed-QP flop count; `frac_executed` is what the kernels actually
@@ -625,7 +625,11 @@ def main():
                      # kernel_avg_ms / achieved / frac: one batch's launch alone (library
                      # defaults, nothing else in flight); the job's own rate with S batches in flight:
                      "achieved_in_flight": flops * B_total * args.steps / elapsed / world / 1e12,
-                     "frac_in_flight": flops * B_total * args.steps / elapsed / world / 1e12 / peak},
+                     "frac_in_flight": flops * B_total * args.steps / elapsed / world / 1e12 / peak,
+                     "frac_in_flight_note": "canonical flop model (SURVEY 8(d), ~2.1e5 flops per solve) at the "
+                                            "in-flight rate: near 1 it is the model that saturates, not the "
+                                            "hardware (the kernels execute ~4e4); frac_executed_in_flight "
+                                            "(PMC) is the hardware figure"},
         "solver": stats,
     }
     if elapsed_g is not None:
@@ -738,7 +742,8 @@ def main():
     # HBM traffic and executed flops per launch from the committed PMC passes of this workload
     # (rocprofv3 --pmc, separate passes; scripts/pmc_hbm.sh, scripts/pmc_flops.sh)
     if not args.lti and not args.f32 and not args.f64 and args.config in ("cfg3", "cfg4"):
-        pmc_into_roofline(line["roofline"], "" if args.config == "cfg3" else "_" + args.config, abytes * B, k_roof_s)
+        pmc_into_roofline(line["roofline"], "" if args.config == "cfg3" else "_" + args.config, abytes * B, k_roof_s,
+                          args.steps / elapsed if S > 1 else None)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
@@ -747,7 +752,7 @@ def main():
 
 
 
-def pmc_into_roofline(roof, suffix, alg_bytes, k_avg_s):
+def pmc_into_roofline(roof, suffix, alg_bytes, k_avg_s, launches_per_s=None):
     """Fill roofline.traffic (HBM bytes per launch, PMC FETCH_SIZE + WRITE_SIZE with the gfx950
     corrections) and the executed-flops fraction from the newest committed profiles/r*/
     pmc_traffic<suffix>.json and pmc_flops<suffix>.json (this workload's own passes).
@@ -767,6 +772,17 @@ def pmc_into_roofline(roof, suffix, alg_bytes, k_avg_s):
         roof["frac_executed"] = (e64 / FP64_PEAK_TFLOPS + e32 / FP32_PEAK_TFLOPS) / 1e12 / k_avg_s
         roof["executed_source"] = (f"{src}: 64 x (2 FMA + ADD + MUL + TRANS) VALU instructions per precision "
                                    "(full-wave count: an upper bound)")
+    # the headline's own executed-flops fraction: the PMC op counters of the in-flight pipeline
+    # (scripts/inflight_run.py: the bench's in-flight settings, every dispatch a batch of the
+    # timed loop's kind) times the launches per second the timed loop achieved
+    fi, src = latest_profile(f"pmc_flops_inflight{suffix}.json")
+    if fi and launches_per_s:
+        e64, e32 = fi["fp64_flops_per_launch"], fi.get("fp32_flops_per_launch", 0.0)
+        roof["executed_flops_per_launch_in_flight"] = {"fp64": e64, "fp32": e32}
+        roof["achieved_executed_in_flight"] = (e64 + e32) * launches_per_s / 1e12
+        roof["frac_executed_in_flight"] = (e64 / FP64_PEAK_TFLOPS + e32 / FP32_PEAK_TFLOPS) * launches_per_s / 1e12
+        roof["executed_in_flight_source"] = (f"{src} (in-flight settings) x {launches_per_s:.4g} launches/s "
+                                             "of the timed loop")
 
 
 REF_LOGGED_SOLVE_MS = 82.6   # mean solve_time_ms of logs/controls_20260208_014109.csv
@@ -1028,16 +1044,16 @@ def bench_other(args, world, rank, local, dist, pre=None):
         # in flight, the MPC branch's first stage runs longer (scripts/r02_s3_caps_cfg.sh:
         # fast cap 9 against the single-batch default 6)
         # (config 5 keeps its side stream in flight: 398-418M against 233M steps/s without)
-        st = W.inflight_settings("cfg5") if S > 1 else dict(W.ALONE)
+        cset = W.inflight_settings("cfg5") if S > 1 else dict(W.ALONE)
         if args.stage_caps:
-            st["caps"] = tuple(int(v) for v in args.stage_caps.split(","))
+            cset["caps"] = tuple(int(v) for v in args.stage_caps.split(","))
         if args.stage_passes:
-            st["passes"] = tuple(int(v) for v in (args.stage_passes + ",0").split(",")[:2])
+            cset["passes"] = tuple(int(v) for v in (args.stage_passes + ",0").split(",")[:2])
         if S > 1:
-            st["cold_start"] = args.cold_start
-        caps = st["caps"]
+            cset["cold_start"] = args.cold_start
+        caps = cset["caps"]
         for i in range(S):
-            rmpc.batch.configure(st, device=local, slot=i)
+            rmpc.batch.configure(cset, device=local, slot=i)
 
         def step(k=0):
             i = k % S
@@ -1056,7 +1072,7 @@ def bench_other(args, world, rank, local, dist, pre=None):
         torch.cuda.synchronize()
         rmpc.batch.configure(dict(W.ALONE, side=bool(args.alone_side)), device=local, slot=0)
         alone_default_s = alone_times(lambda: step(0), torch.cuda.current_stream(), args.steps)[0] / 1e3
-        rmpc.batch.configure(st, device=local, slot=0)
+        rmpc.batch.configure(cset, device=local, slot=0)
     k_roof_s = alone_default_s or k_avg_s     # the roofline's launch: one batch alone, library defaults
     elapsed, _ = W.aggregate(dist, elapsed, [], device=coll_device(args, dev))
     line = {"metric": metric, "value": B_total * args.steps / elapsed,

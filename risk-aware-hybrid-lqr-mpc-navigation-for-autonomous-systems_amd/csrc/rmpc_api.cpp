@@ -778,17 +778,22 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
         }
         for (int i = 0; i < ncap; i++) {
             HIP_TRY(c->pass_list[i].ensure((size_t)B * sizeof(int32_t)));
-            HIP_TRY(c->pass_sets[i].ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
+            HIP_TRY(c->pass_sets[i].ensure((size_t)B * (p->horizon + nb + 1 + RMPC_REC_HIST) * sizeof(uint32_t)));
             MpcFastArgs ai = a;
             ai.pdas_cap = caps[i];
             ai.retry = (int32_t *)c->pass_list[i].p;
             ai.retry_count = cnt + 2 + i;
             ai.retry_sets = (uint32_t *)c->pass_sets[i].p;
+            ai.rec_hist = 1;               // records with the cycle history; cycling robots to the tail
+            ai.cyc = a.retry;
+            ai.cyc_count = a.retry_count;
+            ai.cyc_sets = a.retry_sets;
             HIP_TRY(rmpc_launch_mpc_fast(ai, p->horizon, bs, prec, s, lti));
             dbg_sync(s, "fast pass");
-            a.index = ai.retry;            // the next pass: that list, from its sets
+            a.index = ai.retry;            // the next pass: that list, from its sets and history
             a.count = ai.retry_count;
             a.warm_sets = ai.retry_sets;
+            a.warm_hist = 1;
         }
         HIP_TRY(rmpc_launch_mpc_fast(a, p->horizon, bs, prec, s, lti));
         // tail: the lane-group Riccati kernel (RMPC_DISABLE_DENSE: no tail stage, A/B only)
@@ -838,6 +843,7 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
             r.index = a.refine;
             r.count = a.refine_count;
             r.warm_sets = a.refine_sets;
+            r.warm_hist = 0;               // (refinement records carry no cycle history)
             // one fp64 solve from the fp32 sets: the robots whose sets it does not certify go
             // to the fp64 tail (config 4: 36.5M against 34.8M solves/s with 4 more solves here,
             // whose slowest waves set the pass's length)

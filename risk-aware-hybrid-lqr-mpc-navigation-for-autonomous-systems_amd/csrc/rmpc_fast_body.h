@@ -403,7 +403,7 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid, int
 #pragma unroll
     for (int i = 0; i < (NB + 7) / 8; i++) Bf.w[i] = 0;
 
-    int it = 0, cert = 0, used = 0;
+    int it = 0, cert = 0, used = 0, cycled = 0;
     T J = 0;
     const int maxit0 = min(p.max_iter, a.pdas_cap);
     unsigned long long tp_b = 0, tp_f = 0, tp0 = a.prof ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -440,7 +440,13 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid, int
 #pragma unroll
         for (int j = 0; j < NB; j++) Bf.set(j, ws[(N + j) * a.B]);
         it = (int)ws[(N + NB) * a.B];
-        if (it > 0) hist0 = set_sig();
+        if (a.warm_hist) {                              // the previous pass's cycle history
+            const uint32_t *h = ws + (size_t)(N + NB + 1) * a.B;
+            hist0 = (uint64_t)h[0] | (uint64_t)h[(size_t)a.B] << 32;
+            hist1 = (uint64_t)h[(size_t)2 * a.B] | (uint64_t)h[(size_t)3 * a.B] << 32;
+            hist2 = (uint64_t)h[(size_t)4 * a.B] | (uint64_t)h[(size_t)5 * a.B] << 32;
+            hist3 = (uint64_t)h[(size_t)6 * a.B] | (uint64_t)h[(size_t)7 * a.B] << 32;
+        } else if (it > 0) hist0 = set_sig();
     } else if (WS && a.prev_sets && a.prev_sets[(size_t)(N + NB) * a.B + b] + 1u == a.prev_stamp) {
         // Warm start from this robot's previous solve (rmpc_ctx_set_warm_start): the PDAS
         // counterpart of the reference's warm_start=True with get_warm_start's one-step shift
@@ -974,7 +980,7 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid, int
         // PDAS cycling: a repeated active-set signature hands the robot to the
         // projected-Newton phase of the next stage
         const uint64_t sig = set_sig();
-        if (sig == hist0 || sig == hist1 || sig == hist2 || sig == hist3) break;
+        if (sig == hist0 || sig == hist1 || sig == hist2 || sig == hist3) { cycled = 1; break; }
         hist3 = hist2; hist2 = hist1; hist1 = hist0; hist0 = sig;
     }
     its_out = it - it_start;
@@ -1048,7 +1054,7 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid, int
         // the next stage takes over: one atomic per wave for the lanes here (exec mask), each
         // lane's slot from its rank among them (per-lane atomics on the one counter serialise:
         // a first pass hands on ~21k robots at once)
-        auto hand_on = [&](int32_t *list, int32_t *count, uint32_t *sets) __attribute__((always_inline)) {
+        auto hand_on = [&](int32_t *list, int32_t *count, uint32_t *sets, bool hist) __attribute__((always_inline)) {
             const uint64_t m = __builtin_amdgcn_read_exec();
             const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             int base = 0;
@@ -1064,10 +1070,18 @@ __device__ __forceinline__ void fast_body(MpcFastArgs a, const unsigned wid, int
 #pragma unroll
                 for (int j = 0; j < NB; j++) ws[(N + j) * a.B] = Bf.get(j);
                 ws[(N + NB) * a.B] = (uint32_t)it;
+                if (hist) {                                   // (an earlier pass: + the cycle history)
+                    uint32_t *h = ws + (size_t)(N + NB + 1) * a.B;
+                    h[0] = (uint32_t)hist0; h[(size_t)a.B] = (uint32_t)(hist0 >> 32);
+                    h[(size_t)2 * a.B] = (uint32_t)hist1; h[(size_t)3 * a.B] = (uint32_t)(hist1 >> 32);
+                    h[(size_t)4 * a.B] = (uint32_t)hist2; h[(size_t)5 * a.B] = (uint32_t)(hist2 >> 32);
+                    h[(size_t)6 * a.B] = (uint32_t)hist3; h[(size_t)7 * a.B] = (uint32_t)(hist3 >> 32);
+                }
             }
         };
-        if (to_refine) hand_on(a.refine, a.refine_count, a.refine_sets);
-        else hand_on(a.retry, a.retry_count, a.retry_sets);
+        if (to_refine) hand_on(a.refine, a.refine_count, a.refine_sets, false);
+        else if (cycled && a.cyc) hand_on(a.cyc, a.cyc_count, a.cyc_sets, false);   // (earlier pass: to the tail)
+        else hand_on(a.retry, a.retry_count, a.retry_sets, a.rec_hist != 0);
         if (a.prof) atomicMax(a.prof + 23, __builtin_amdgcn_s_memtime() - t_entry);   // longest lane, entry to exit
         return;
     }

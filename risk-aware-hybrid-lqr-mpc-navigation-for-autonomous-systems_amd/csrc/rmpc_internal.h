@@ -86,7 +86,17 @@ struct MpcFastArgs {
     int prev_shift;
     uint32_t prev_stamp;
     int init_zc;                     // cold start: hinge rows violated by the free response start active
+    // Multi-pass stage (rmpc_ctx_set_stage_passes).  An earlier pass's records (retry_sets) also
+    // carry the cycle history after the iteration word -- RMPC_REC_HIST words, the four
+    // newest active-set signatures as lo/hi pairs (rec_hist) -- and the next pass restores it
+    // (warm_hist), so a continued robot detects a cycle exactly when the one-pass stage would;
+    // a robot whose sets cycle in an earlier pass goes straight to the tail's list (cyc: list,
+    // counter, records), as it would from the one-pass stage.  Null / 0: off.
+    int rec_hist, warm_hist;
+    int32_t *cyc, *cyc_count;
+    uint32_t *cyc_sets;
 };
+#define RMPC_REC_HIST 8
 // LDS slot.  The LDS-using kernels of the MPC pipeline (the lane-per-robot stage, the lane-group
 // tail, the generic kernel's leftover list) each run one wave per SIMD, four per CU, and with
 // batches in flight they replace each other on the CUs.  A CU allocates each workgroup's LDS as

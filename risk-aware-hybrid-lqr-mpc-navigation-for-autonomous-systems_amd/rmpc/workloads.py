@@ -34,9 +34,11 @@ CONFIGS = {
 # same under every setting).  tests/test_gpu_headline.py runs exactly these.  Measured choices:
 # caps (9, 3) for config 3 (profiles/r05/session_46-48), (13, 4) LTI, (14, 6) config 4, (9, 4)
 # config 5 (its MPC branch); zero-correction first sets in flight (session_27, _49); side
-# streams off in flight except config 5's LQR branch (profiles/r03/ab_side_streams_in_flight).
+# streams off in flight except config 5's LQR branch (profiles/r03/ab_side_streams_in_flight);
+# config 3's stage 1 in two passes, the first one PDAS solve long (profiles/r06: +2.6% at the
+# driver's command over five pairs, +3% at 100 steps; configs 4 and LTI lose with passes).
 INFLIGHT = {
-    "cfg3": dict(caps=(9, 3), cold_start=1, passes=(0, 0), side=False),
+    "cfg3": dict(caps=(9, 3), cold_start=1, passes=(1, 0), side=False),
     "lti": dict(caps=(13, 4), cold_start=1, passes=(0, 0), side=False),
     "cfg4": dict(caps=(14, 6), cold_start=1, passes=(0, 0), side=False),
     "cfg5": dict(caps=(9, 4), cold_start=1, passes=(0, 0), side=True),

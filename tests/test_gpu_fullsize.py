@@ -483,3 +483,52 @@ def test_tail_multi_round_loop_bounds_checked(rm, monkeypatch, capfd):
     assert grids[1] < 128            # config 3's ~900 tail rounds on the 64-robot call's small grid
     for o in outs:
         assert np.all(o["status"] == 0)
+
+
+@pytest.mark.parametrize("cold", [0, 1])
+def test_stage_passes_give_the_one_pass_bits(rm, cold):
+    """rmpc_ctx_set_stage_passes: the lane-per-robot stage in two or three passes, each later
+    pass continuing only the uncertified robots from their records (active sets, iteration count
+    and cycle history; a robot whose sets cycle goes straight to the tail) -- the same iterate
+    path as one pass, so every output of config 3's full batch is bitwise the one-pass output,
+    at the in-flight caps (9, 3), with empty and with zero-correction first sets; and config 4's
+    fp32 request (paired lanes, fp64 refinement) at 8192 robots the same way."""
+    import torch
+    from rmpc import workloads as W
+    dev = torch.device("cuda:0")
+
+    def run(p, x0h, xrh, urh, obs_list, caps, passes, slot):
+        x0, xr, ur = (torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (x0h, xrh, urh))
+        obs = torch.tensor(obs_list, dtype=torch.float64, device=dev).reshape(-1, 3)
+        B, n = x0.shape[0], xrh.shape[1] - 1
+        o = dict(u0=torch.empty(B, 2, dtype=torch.float64, device=dev),
+                 u_seq=torch.empty(B, n, 2, dtype=torch.float64, device=dev),
+                 x_pred=torch.empty(B, n + 1, 3, dtype=torch.float64, device=dev),
+                 cost=torch.empty(B, dtype=torch.float64, device=dev),
+                 status=torch.empty(B, dtype=torch.int32, device=dev),
+                 slack_used=torch.empty(B, dtype=torch.uint8, device=dev),
+                 iters=torch.empty(B, dtype=torch.int32, device=dev))
+        rm.batch.configure(dict(caps=caps, cold_start=cold, passes=passes, side=True), slot=slot)
+        rm.batch.mpc_solve_batch_dev(p, x0, xr, ur, obs, o, step_count=torch.full((B,), 10, dtype=torch.int32,
+                                                                                 device=dev), slot=slot)
+        torch.cuda.synchronize()
+        return {k: v.cpu().numpy() for k, v in o.items()}
+
+    x0, xr, ur = cfg3_inputs()
+    p = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+    one = run(p, x0, xr, ur, ompc.default_obstacles(), (9, 3), (0, 0), 16)
+    assert np.all(one["status"] == 0) and (one["iters"] > 9).sum() > 500
+    for passes in ((1, 0), (1, 3), (2, 5)):
+        got = run(p, x0, xr, ur, ompc.default_obstacles(), (9, 3), passes, 17)
+        for k in one:
+            np.testing.assert_array_equal(got[k], one[k], err_msg=f"{passes} {k}")
+    B4, N4 = 8192, 30
+    idx = np.arange(B4)
+    xr4, ur4 = rm.batch.figure8_batch(W.t0_at(idx, B4), N4 + 1)
+    x04 = xr4[:, 0] + W.noise_at(idx, W.CONFIGS["cfg4"]["seed"])
+    p4 = rm._native.mpc_params(N4, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02, precision=1)
+    one = run(p4, x04, xr4, ur4, W.UNION8_OBS, (14, 6), (0, 0), 16)
+    assert np.all(one["status"] == 0)
+    got = run(p4, x04, xr4, ur4, W.UNION8_OBS, (14, 6), (2, 6), 17)
+    for k in one:
+        np.testing.assert_array_equal(got[k], one[k], err_msg=f"cfg4 {k}")
