@@ -718,6 +718,12 @@ def main():
             "sample": f"{nsamp} robots (every {B // nsamp}th) of the same workload x {reps} reps "
                       f"(oracle/c/rmpc_cpu.c, OpenMP, same algorithm, stage caps {caps} and outputs)",
             "single_thread_solves_per_s": n1 / t1,
+            # SURVEY 8(d) names OpenMP over all host cores; the job may use its share only (gpurun:
+            # OMP_NUM_THREADS=16 of the machine's hardware threads, shared by 8 GPUs' jobs), so the
+            # all-core figure is the measured per-thread rate scaled to every hardware thread --
+            # a projection (perfect scaling, no SMT loss), never measured here
+            "all_host_threads_projected": {"value": nsamp * reps / t_cpu / threads * (os.cpu_count() or threads),
+                                           "threads": os.cpu_count(), "kind": "projection from the measured rate"},
             "reference_published_ms_per_solve": 82.6,
             "reference_published_note": "CVXPY/OSQP N=6 logged mean, hardware unstated (BASELINE.md)",
             "host": host_info()}

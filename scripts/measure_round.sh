@@ -8,7 +8,7 @@
 #   (outputs under gpurun_out/<tag>_*; the PMC jsons are copied into the profiles dir, where
 #   bench.py finds the newest; one phase per gpurun call keeps each call under its time limit)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
-tag=${1:-m}; rdir=${2:-profiles/r05}; phase=${3:-all}
+tag=${1:-m}; rdir=${2:-profiles/r06}; phase=${3:-all}
 mkdir -p gpurun_out $rdir
 step() { echo "== $(date +%T) $*"; }
 prof() {   # prof <name> <bench args...>: rocprofv3 kernel trace + stats of a short bench run
@@ -32,6 +32,15 @@ if [ $phase = all ] || [ $phase = pmc ]; then
 pmc "" mpc_ltv_fast_kernel --inflight 1
 pmc _cfg4 "mpc_ltv_fast_kernel<30, 1, float" --config cfg4 --inflight 1
 pmc _cfg5 hybrid_decide_kernel --config cfg5 --inflight 1
+# the headline's own executed flops: the op counters of the in-flight pipeline alone
+# (scripts/inflight_run.py, the bench's in-flight settings; entry = a kernel run once per call)
+step pmc flops in flight
+GPU_MAX_HW_QUEUES=16 PROG="scripts/inflight_run.py --steps 16" bash scripts/pmc_flops.sh ${tag}_fli "mpc_group_kernel<20" \
+  > gpurun_out/${tag}_pmc_fli.log 2>&1 || { tail gpurun_out/${tag}_pmc_fli.log; exit 1; }
+cp gpurun_out/${tag}_fli_flops.json $rdir/pmc_flops_inflight.json
+GPU_MAX_HW_QUEUES=16 PROG="scripts/inflight_run.py --steps 16 --config cfg4" bash scripts/pmc_flops.sh ${tag}_fli4 "mpc_ltv_fast_kernel<30, 1, float" \
+  > gpurun_out/${tag}_pmc_fli4.log 2>&1 || { tail gpurun_out/${tag}_pmc_fli4.log; exit 1; }
+cp gpurun_out/${tag}_fli4_flops.json $rdir/pmc_flops_inflight_cfg4.json
 step smoke
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 || { cat gpurun_out/${tag}_smoke.log; exit 1; }
 fi

@@ -154,12 +154,34 @@ def analyse(d, us_per_tick, label):
     return rep
 
 
+def busy_profile(d, us_per_tick, bin_us):
+    """Busy SIMD fraction per time bin over the window (all kernels): dips show the moments the
+    chip waits for work (e.g. every stream's tail running at once)."""
+    t_lo = d["t0"].min()
+    nb = int(np.ceil((d["t1"].max() - t_lo) * us_per_tick / bin_us)) + 1
+    busy = np.zeros(nb)
+    a = (d["t0"] - t_lo) * us_per_tick / bin_us
+    b = (d["t1"] - t_lo) * us_per_tick / bin_us
+    for x, y in zip(a, b):        # add each wave's coverage of the bins
+        i0, i1 = int(x), int(y)
+        if i0 == i1:
+            busy[i0] += y - x
+        else:
+            busy[i0] += i0 + 1 - x
+            busy[i0 + 1:i1] += 1
+            busy[i1] += y - i1
+    n_simd = np.unique(d["simd"]).size
+    return [round(float(v), 3) for v in busy / n_simd]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--inflight", type=int, default=8)
-    ap.add_argument("--caps", default="9,4")
+    ap.add_argument("--caps", default=None, help="F,T: stage caps instead of rmpc.workloads.INFLIGHT's")
+    ap.add_argument("--passes", default=None, help="C1[,C2]: stage-1 passes instead of INFLIGHT's")
+    ap.add_argument("--bin-us", type=float, default=20.0, help="bin width of the busy-SIMD profile")
     ap.add_argument("--out", default="gpurun_out/wl.npz")
     ap.add_argument("--cap-records", type=int, default=1 << 23)
     ap.add_argument("--cold-start", type=int, default=1, help="in-flight contexts' rmpc_ctx_set_cold_start mode")
@@ -192,11 +214,15 @@ def main():
     obs = torch.tensor(obs_list, dtype=torch.float64, device=dev).reshape(-1, 3)
     p = rmpc._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(S - 1)]
-    caps = tuple(int(v) for v in args.caps.split(",")) if S > 1 else (0, 0)
+    cset = W.inflight_settings("cfg3") if S > 1 else dict(W.ALONE)
+    if args.caps:
+        cset["caps"] = tuple(int(v) for v in args.caps.split(","))
+    if args.passes:
+        cset["passes"] = tuple(int(v) for v in (args.passes + ",0").split(",")[:2])
+    if S > 1:
+        cset["cold_start"] = args.cold_start
     for i in range(S):
-        rmpc.batch.set_stage_caps(*caps, device=0, slot=i)
-        rmpc.batch.set_side_stream(S == 1, device=0, slot=i)
-        rmpc.batch.set_cold_start(args.cold_start if S > 1 else 0, device=0, slot=i)
+        rmpc.batch.configure(cset, device=0, slot=i)
 
     def step(k):
         i = k % S
@@ -209,9 +235,7 @@ def main():
     saved = {}
     for label, nsteps, slots in (("inflight", args.steps, S), ("alone_default_caps", args.steps, 1)):
         if label.startswith("alone"):
-            rmpc.batch.set_stage_caps(0, 0, device=0, slot=0)
-            rmpc.batch.set_cold_start(0, device=0, slot=0)
-            rmpc.batch.set_side_stream(True, device=0, slot=0)
+            rmpc.batch.configure(W.ALONE, device=0, slot=0)
         run = (lambda k: step(k)) if slots > 1 else (lambda k: step(0))
         for k in range(max(args.warmup, S)):
             run(k)
@@ -230,6 +254,8 @@ def main():
         # s_memrealtime is 100 MHz on MI300-class parts; cross-check against the host wall clock
         us_per_tick = 0.01
         rep = analyse(d, us_per_tick, label)
+        rep["settings"] = {k: list(v) if isinstance(v, tuple) else v for k, v in cset.items()} if slots > 1 else "library defaults"
+        rep["busy_profile"] = busy_profile(d, us_per_tick, args.bin_us)
         rep["host_wall_us"] = wall * 1e6
         rep["records"] = int(n)
         rep["wall_over_span"] = wall * 1e6 / (span_ticks * us_per_tick)
