@@ -166,6 +166,13 @@ int rmpc_ctx_set_stage_caps(RmpcCtx *ctx, int32_t fast_cap, int32_t tail_cap);
  * lane slots that certified robots leave idle in a one-pass wave (HISTORY.md section 11).
  * Caps in [0, 64], second_cap above first_cap or 0. */
 int rmpc_ctx_set_stage_passes(RmpcCtx *ctx, int32_t first_cap, int32_t second_cap);
+/* Lanes per robot in the lane-per-robot stage on this context (a performance setting; results
+ * are the same QP optimum): 0 (default) = the library's choice, which pairs two lanes per
+ * robot in the fp32 N = 30, 8-obstacle stage (BASELINE config 4: the rows split over the pair,
+ * and 32768 robots then fill every SIMD of one GPU); 1 = one lane per robot there too (half the
+ * waves and no duplicated recursion: with batches in flight the other batches fill the SIMDs,
+ * config 4 +13%; one batch alone -20%); 2 = paired.  Other instances have one form. */
+int rmpc_ctx_set_lanes_per_robot(RmpcCtx *ctx, int32_t lanes);
 /* Side stream on this context (a performance setting; results are identical): on (default),
  * a pipeline's independent branch -- the fp64 refinement of an fp32 request beside the tail,
  * the hybrid step's LQR branch beside the MPC branch -- runs on a second stream of the context,

@@ -88,6 +88,7 @@ struct RmpcCtx {
     // multi-pass lane-per-robot stage: the earlier passes' hand-on lists and their sets
     DevBuf pass_list[2], pass_sets[2];
     int passes[2] = {0, 0};           // rmpc_ctx_set_stage_passes: the earlier passes' caps (0: none)
+    int lanes = 0;                    // rmpc_ctx_set_lanes_per_robot (0: the library default)
     GroupDiag gdiag;           // lane-group tail diagnostics (RMPC_GROUP_CHECK, RMPC_DENSE_PROF=2)
     // per tail launch site, the list length its last launch saw (host-mapped words the tail
     // kernel writes; -1 before the first): the next launch's grid (rmpc_launch_mpc_group)
@@ -371,6 +372,14 @@ int rmpc_ctx_set_stage_passes(RmpcCtx *c, int32_t first_cap, int32_t second_cap)
         sc->passes[0] = c->passes[0];
         sc->passes[1] = c->passes[1];
     }
+    return RMPC_OK;
+}
+
+int rmpc_ctx_set_lanes_per_robot(RmpcCtx *c, int32_t lanes) {
+    if (!c) return fail(RMPC_EINVAL, "ctx is NULL");
+    if (lanes < 0 || lanes > 2) return fail(RMPC_EINVAL, "lanes per robot %d: 0 (default), 1 or 2", lanes);
+    c->lanes = lanes;
+    for (auto &sc : c->sub) sc->lanes = lanes;
     return RMPC_OK;
 }
 
@@ -697,6 +706,7 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
                      : c->fast_cap > 0        ? c->fast_cap
                                               : (p->horizon <= 20 ? (lti ? 9 : 7) : 12);
         a.init_zc = c->cold_rows ? 1 : 0;  // rmpc_ctx_set_cold_start
+        a.lanes = c->lanes;                // rmpc_ctx_set_lanes_per_robot
         // the tail continues from each handed-on robot's sets (retry_sets)
         HIP_TRY(c->retry_sets.ensure((size_t)B * (p->horizon + nb + 1) * sizeof(uint32_t)));
         a.retry_sets = (uint32_t *)c->retry_sets.p;

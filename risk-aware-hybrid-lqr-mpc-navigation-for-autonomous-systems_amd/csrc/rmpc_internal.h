@@ -95,6 +95,9 @@ struct MpcFastArgs {
     int rec_hist, warm_hist;
     int32_t *cyc, *cyc_count;
     uint32_t *cyc_sets;
+    // lanes per robot (rmpc_ctx_set_lanes_per_robot): 1 = one lane per robot where an instance
+    // has both forms (the fp32 N = 30 8-obstacle stage); 0 = the default (paired there)
+    int lanes;
 };
 #define RMPC_REC_HIST 8
 // LDS slot.  The LDS-using kernels of the MPC pipeline (the lane-per-robot stage, the lane-group

@@ -69,7 +69,10 @@ hipError_t rmpc_launch_mpc_fast(const MpcFastArgs &a, int N, int bs, int prec, h
     } else if (prec == RMPC_F32) {
         // paired lanes for the 8-obstacle N = 30 instance
         const dim3 grid2((unsigned)((n + RMPC_WAVE / 2 - 1) / (RMPC_WAVE / 2)));
-        if (bs == 1 && N == 30 && a.no == 8 && rmpc_knob("RMPC_F32_PR1"))      // (A/B: one lane per robot)
+        // one lane per robot on request (rmpc_ctx_set_lanes_per_robot): half the waves, no
+        // duplicated recursion -- with batches in flight the other batches fill the SIMDs this
+        // leaves idle (config 4 in flight +13%; one batch alone -20%)
+        if (bs == 1 && N == 30 && a.no == 8 && a.lanes == 1)
             FK((mpc_ltv_fast_kernel<30, 1, float, false, 8, 1>), grid, lds);
         else if (bs == 1 && N == 30 && a.no == 8) FK((mpc_ltv_fast_kernel<30, 1, float, false, 8, 2>), grid2, lds2);
         else if (bs == 1 && N == 20) FK((mpc_ltv_fast_kernel<20, 1, float, false>), grid, lds);

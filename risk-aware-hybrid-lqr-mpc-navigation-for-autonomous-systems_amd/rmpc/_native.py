@@ -81,6 +81,7 @@ _PROTOS = {
     "rmpc_ctx_set_timing": [_vp, _i32],
     "rmpc_ctx_set_stage_caps": [_vp, _i32, _i32],
     "rmpc_ctx_set_stage_passes": [_vp, _i32, _i32],
+    "rmpc_ctx_set_lanes_per_robot": [_vp, _i32],
     "rmpc_ctx_set_side_stream": [_vp, _i32],
     "rmpc_ctx_set_cold_start": [_vp, _i32],
     "rmpc_ctx_set_warm_start": [_vp, _i32],

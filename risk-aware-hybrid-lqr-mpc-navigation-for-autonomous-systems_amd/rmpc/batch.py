@@ -243,12 +243,22 @@ def set_stage_passes(first_cap=0, second_cap=0, device=0, slot=0):
           "rmpc_ctx_set_stage_passes")
 
 
+def set_lanes_per_robot(lanes=0, device=0, slot=0):
+    """Lanes per robot in the lane-per-robot stage (rmpc_ctx_set_lanes_per_robot): 0 the
+    library's choice (paired lanes for the fp32 N = 30, 8-obstacle stage), 1 one lane per robot,
+    2 paired.  Same optimum."""
+    lib = nat.load()
+    check(lib.rmpc_ctx_set_lanes_per_robot(nat.context(device, slot), int(lanes)), "rmpc_ctx_set_lanes_per_robot")
+
+
 def configure(settings, device=0, slot=0):
     """All performance settings of one context at once: `settings` a dict with caps (fast,
-    tail), cold_start, passes (first, second) and side (rmpc.workloads.INFLIGHT / ALONE)."""
+    tail), cold_start, passes (first, second), lanes (per robot) and side
+    (rmpc.workloads.INFLIGHT / ALONE)."""
     set_stage_caps(*settings["caps"], device=device, slot=slot)
     set_cold_start(settings["cold_start"], device=device, slot=slot)
     set_stage_passes(*settings["passes"], device=device, slot=slot)
+    set_lanes_per_robot(settings.get("lanes", 0), device=device, slot=slot)
     set_side_stream(settings["side"], device=device, slot=slot)
 
 

@@ -36,15 +36,17 @@ CONFIGS = {
 # config 5 (its MPC branch); zero-correction first sets in flight (session_27, _49); side
 # streams off in flight except config 5's LQR branch (profiles/r03/ab_side_streams_in_flight);
 # config 3's stage 1 in two passes, the first one PDAS solve long (profiles/r06: +2.6% at the
-# driver's command over five pairs, +3% at 100 steps; configs 4 and LTI lose with passes).
+# driver's command over five pairs, +3% at 100 steps; configs 4 and LTI lose with passes);
+# config 4's fp32 stage at one lane per robot in flight (profiles/r06: +13% in flight, three
+# pairs; its one batch alone keeps the paired lanes, -20% otherwise).
 INFLIGHT = {
-    "cfg3": dict(caps=(9, 3), cold_start=1, passes=(1, 0), side=False),
-    "lti": dict(caps=(13, 4), cold_start=1, passes=(0, 0), side=False),
-    "cfg4": dict(caps=(14, 6), cold_start=1, passes=(0, 0), side=False),
-    "cfg5": dict(caps=(9, 4), cold_start=1, passes=(0, 0), side=True),
+    "cfg3": dict(caps=(9, 3), cold_start=1, passes=(1, 0), lanes=0, side=False),
+    "lti": dict(caps=(13, 4), cold_start=1, passes=(0, 0), lanes=0, side=False),
+    "cfg4": dict(caps=(14, 6), cold_start=1, passes=(0, 0), lanes=1, side=False),
+    "cfg5": dict(caps=(9, 4), cold_start=1, passes=(0, 0), lanes=0, side=True),
 }
 # one batch at a time: the library's defaults
-ALONE = dict(caps=(0, 0), cold_start=0, passes=(0, 0), side=True)
+ALONE = dict(caps=(0, 0), cold_start=0, passes=(0, 0), lanes=0, side=True)
 
 
 def inflight_settings(config, lti=False):

@@ -1,9 +1,9 @@
 """Minimal in-flight run of the MPC pipeline for counter passes (diagnostics): S fleets of a
 BASELINE configuration in flight on their own contexts and streams, exactly as bench.py's timed
-loop sets them up (in-flight stage caps, zero-correction first sets, side streams off), and
-nothing else -- no one-batch-alone legs, no host-pointer or closed-loop calls -- so that every
+loop sets them up (rmpc.workloads.INFLIGHT: stage caps, zero-correction first sets, stage
+passes, lanes per robot, side streams), and nothing else -- no one-batch-alone legs, no host-pointer or closed-loop calls -- so that every
 dispatch of the MPC kernels in a rocprofv3 pass belongs to the in-flight pipeline.
-Usage: [RMPC_DIAG=1 RMPC_FAST_SPLIT=1] python scripts/inflight_run.py [--config cfg3|cfg4]
+Usage: python scripts/inflight_run.py [--config cfg3|cfg4]
        [--inflight 8] [--steps 16] [--warmup 8] [--caps F,T] [--passes c1[,c2]]
 Prints one JSON line: wall-clock rate of the timed steps and the solver status counts."""
 import argparse
@@ -57,18 +57,13 @@ def main():
     p = rmpc._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02,
                                 precision=1 if f32 else 0)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(S - 1)]
-    caps = (14, 6) if f32 else (9, 3)
+    cset = W.inflight_settings(args.config) if S > 1 else dict(W.ALONE)     # bench.py's settings
     if args.caps:
-        caps = tuple(int(v) for v in args.caps.split(","))
-    if S == 1:
-        caps = (0, 0)
-    passes = tuple(int(v) for v in args.passes.split(",")) if args.passes else None
+        cset["caps"] = tuple(int(v) for v in args.caps.split(","))
+    if args.passes:
+        cset["passes"] = tuple(int(v) for v in (args.passes + ",0").split(",")[:2])
     for i in range(S):
-        rmpc.batch.set_stage_caps(*caps, device=0, slot=i)
-        rmpc.batch.set_side_stream(S == 1, device=0, slot=i)
-        rmpc.batch.set_cold_start(1 if S > 1 else 0, device=0, slot=i)
-        if passes:
-            rmpc.batch.set_stage_passes(*passes, device=0, slot=i)
+        rmpc.batch.configure(cset, device=0, slot=i)
 
     def step(k):
         i = k % S
@@ -86,8 +81,8 @@ def main():
     el = time.perf_counter() - t
     st = torch.cat([o["status"] for o in outs]).cpu().numpy()
     its = torch.cat([o["iters"] for o in outs]).cpu().numpy()
-    print(json.dumps({"config": args.config, "inflight": S, "steps": args.steps, "caps": caps, "passes": passes,
-                      "split_knob": os.environ.get("RMPC_FAST_SPLIT"), "value": B * args.steps / el,
+    print(json.dumps({"config": args.config, "inflight": S, "steps": args.steps, "settings": cset,
+                      "value": B * args.steps / el,
                       "ms_per_step": el / args.steps * 1e3, "optimal": int((st == 0).sum()), "robots": int(st.size),
                       "iters_mean": float(its.mean())}), flush=True)
 

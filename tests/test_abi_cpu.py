@@ -75,6 +75,7 @@ def test_null_context_is_rejected(lib):
     assert lib.rmpc_ctx_set_side_stream(None, 1) == -1
     assert lib.rmpc_ctx_set_cold_start(None, 1) == -1
     assert lib.rmpc_ctx_set_stage_passes(None, 1, 0) == -1
+    assert lib.rmpc_ctx_set_lanes_per_robot(None, 1) == -1
     assert lib.rmpc_ctx_set_warm_start(None, 1) == -1
 
 
