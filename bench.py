@@ -385,14 +385,17 @@ def main():
                     help="keep the library's side streams on the in-flight contexts (A/B; default off there)")
     ap.add_argument("--inflight", type=int, default=None,
                     help="batches in flight at once, each on its own stream with its own solver "
-                         "context and outputs (step k runs on stream k mod S); default 8, config 2 3 "
-                         "(its ~7 us LQR launches are host-bound: 758M controls/s at 3 against 380M at 8)")
+                         "context and outputs (step k runs on stream k mod S); default 8; config 3 "
+                         "(solve_with_ltv) 10 on 32 hardware queues (profiles/r06: +1.9%% at 20 steps, "
+                         "+3.7%% at 100 over 8 on 16); config 2 3 (its ~7 us LQR launches are "
+                         "host-bound: 758M controls/s at 3 against 380M at 8)")
     ap.add_argument("--cold-start", type=int, default=1, choices=[0, 1],
                     help="in-flight contexts' first active sets (rmpc_ctx_set_cold_start): 1 zero-correction rows")
-    ap.add_argument("--hw-queues", type=int, default=16,
+    ap.add_argument("--hw-queues", type=int, default=None,
                     help="hardware queues per process (GPU_MAX_HW_QUEUES, at most 32; HIP's default is 4): "
                          "each batch in flight needs a queue of its own, or two fleets' streams share one "
-                         "in-order queue (0: leave the environment's setting)")
+                         "in-order queue (0: leave the environment's setting); default 16, config 3 "
+                         "(solve_with_ltv) 32")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N>1 on a one-GPU box: every rank on cuda:0, gloo collectives through host "
                          "tensors (exercises the multi-rank bench flow; not a scaling number)")
@@ -405,8 +408,11 @@ def main():
                     help="--selftest: this rank exits with status 3 after joining the group (launcher test)")
     args = ap.parse_args()
     args.inflight_given = args.inflight is not None
+    cfg3_ltv = args.config == "cfg3" and not args.lti
     if args.inflight is None:
-        args.inflight = 3 if args.config == "cfg2" else 8
+        args.inflight = 3 if args.config == "cfg2" else (10 if cfg3_ltv else 8)
+    if args.hw_queues is None:
+        args.hw_queues = 32 if cfg3_ltv else 16
     if args.alone_side is None:
         args.alone_side = 0 if args.hw_queues > 4 else 1
     # (before anything initialises HIP: the setting is read once per process; spawned ranks
