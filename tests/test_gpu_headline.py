@@ -6,7 +6,7 @@ context and stream, every context configured with rmpc.workloads.INFLIGHT[config
 zero-correction first sets, stage-1 passes, side stream).  Here eight slots on eight streams run
 the full batch of each configuration with exactly those settings -- two rounds of launches for
 the MPC configurations, so each slot's second launch overlaps the others' -- and:
-  - the eight outputs are bitwise equal to a solve alone on a ninth context with the same
+  - the ten outputs are bitwise equal to a solve alone on a ninth context with the same
     settings (the contexts share no scratch, and in-flight overlap changes no result);
   - config 3: every robot's u0, u_seq and x_pred (the outputs mpc_controller.py:497-505
     returns) against the C port at 1e-9, and every robot of hard_cfg3.npz (the tail robots
@@ -29,8 +29,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "gol
 from make_hard_fixtures import cfg3_inputs, cfg5_inputs  # noqa: E402
 
 pytestmark = pytest.mark.gpu
-SLOTS = list(range(40, 48))     # eight in-flight contexts of their own (other tests use 0-13)
-ALONE = 48
+SLOTS = list(range(40, 50))     # ten in-flight contexts of their own (bench.py runs config 3 at 10; other tests use 0-18)
+ALONE = 50
 
 
 @pytest.fixture(scope="module")
