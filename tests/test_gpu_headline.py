@@ -1,12 +1,13 @@
 """The headline's exact in-flight settings, pinned (review item: the bench's own settings had
 no GPU test of their own).
 
-bench.py times BASELINE configs 3, 4 and 5 with eight batches in flight, each on its own
-context and stream, every context configured with rmpc.workloads.INFLIGHT[config] (stage caps,
-zero-correction first sets, stage-1 passes, side stream).  Here eight slots on eight streams run
+bench.py times BASELINE configs 3, 4 and 5 with ten (config 3) or eight batches in flight, each
+on its own context and stream, every context configured with rmpc.workloads.INFLIGHT[config]
+(stage caps, zero-correction first sets, stage-1 passes, lanes per robot, side stream).  Here ten
+slots on ten streams run
 the full batch of each configuration with exactly those settings -- two rounds of launches for
 the MPC configurations, so each slot's second launch overlaps the others' -- and:
-  - the ten outputs are bitwise equal to a solve alone on a ninth context with the same
+  - the ten outputs are bitwise equal to a solve alone on an eleventh context with the same
     settings (the contexts share no scratch, and in-flight overlap changes no result);
   - config 3: every robot's u0, u_seq and x_pred (the outputs mpc_controller.py:497-505
     returns) against the C port at 1e-9, and every robot of hard_cfg3.npz (the tail robots
@@ -40,7 +41,7 @@ def rm(gpu_lib):
 
 
 def _mpc_inflight(rm, settings, p, x0h, xrh, urh, obs_list, step0, rounds=2):
-    """Eight slots in flight (two rounds) and one solve alone, all configured with `settings`;
+    """Ten slots in flight (two rounds) and one solve alone, all configured with `settings`;
     returns (alone outputs, [slot outputs]) as numpy dicts."""
     import torch
     dev = torch.device("cuda:0")
