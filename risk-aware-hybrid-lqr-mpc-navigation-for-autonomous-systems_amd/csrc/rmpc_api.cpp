@@ -129,10 +129,6 @@ struct RmpcCtx {
     // the robots it hands on go to a list of their own (retry_r, sets retry_sets_r)
     hipEvent_t rev[2] = {nullptr, nullptr};
     DevBuf retry_r, retry_sets_r;
-    // tail at high priority (RMPC_TAIL_HI, A/B): the tail and generic kernels on a stream of the
-    // device's greatest priority, forked from and joined back to the call's stream (tev)
-    hipStream_t tstream = nullptr;
-    hipEvent_t tev[2] = {nullptr, nullptr};
     // Consecutive calls share state on the device (list counters zeroed by the previous
     // pipeline, the hybrid step's counter pairs, warm-start sets and stamps), which is correct
     // in stream order.  A call on another stream than the previous call's first waits for that
@@ -306,12 +302,6 @@ int rmpc_ctx_destroy(RmpcCtx *c) {
     for (auto &e : c->hev)
         if (e) (void)hipEventDestroy(e);
     for (auto &e : c->rev)
-        if (e) (void)hipEventDestroy(e);
-    if (c->tstream) {
-        (void)hipStreamSynchronize(c->tstream);
-        (void)hipStreamDestroy(c->tstream);
-    }
-    for (auto &e : c->tev)
         if (e) (void)hipEventDestroy(e);
     if (c->last_ev) (void)hipEventDestroy(c->last_ev);
     c->retry_r.release();
@@ -888,44 +878,12 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
         // tail PDAS cap before projected Newton (sweeps: 4 at N <= 20, 6 beyond -- config 4)
         const int tail_cap = c->tail_cap > 0 ? c->tail_cap : (p->horizon <= 20 ? 4 : 6);
         // (a refined fp32 request takes the fp64 tail: it returns fp64 optima only)
-        // (RMPC_TAIL_HI, A/B: the tail and generic kernels on a high-priority stream, forked here
-        // and joined back before the call returns -- the stream contract is unchanged)
-        hipStream_t ts = s;
-        if (!refine_side && !c->timing && !prof && rmpc_knob("RMPC_TAIL_HI")) {
-            if (!c->tstream) {
-                int lo = 0, hi = 0;
-                HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-                HIP_TRY(hipStreamCreateWithPriority(&c->tstream, hipStreamNonBlocking, hi));
-            }
-            for (auto &e : c->tev)
-                if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            HIP_TRY(hipEventRecord(c->tev[0], s));
-            HIP_TRY(hipStreamWaitEvent(c->tstream, c->tev[0], 0));
-            ts = c->tstream;
-        }
-        auto tjoin = [&]() -> hipError_t {   // the high-priority branch -> the call's stream
-            if (ts == s) return hipSuccess;
-            hipError_t e = hipEventRecord(c->tev[1], ts);
-            if (e == hipSuccess) e = hipStreamWaitEvent(s, c->tev[1], 0);
-            if (e != hipSuccess) (void)hipStreamSynchronize(ts);
-            ts = s;
-            return e;
-        };
-#define HIP_TRY_T(expr)                      \
-    do {                                     \
-        const hipError_t et_ = (expr);       \
-        if (et_ != hipSuccess) {             \
-            (void)join();                    \
-            (void)tjoin();                   \
-            HIP_TRY(et_);                    \
-        }                                    \
-    } while (0)
         if (group_tail) {
             int32_t *cnt2 = cnt + 8;
-            HIP_TRY_T(rmpc_launch_mpc_group(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs, uref_rows,
+            HIP_TRY_J(rmpc_launch_mpc_group(d, p->horizon, bs, n_obs, B, x0, x_refs, ref_rows, u_refs, uref_rows,
                                             obstacles, step_count, u0, u_seq, x_pred, cost, status, slack_used,
                                             iters, left, left_n, (int32_t *)c->retry2.p, cnt2, tail_cap,
-                                            a.retry_sets, ts, pc, lti, &c->gdiag, a.prev_sets, a.prev_stamp,
+                                            a.retry_sets, s, pc, lti, &c->gdiag, a.prev_sets, a.prev_stamp,
                                             hint_d[0], hint_p[0]));
             HIP_TRY(join());               // the refinement, before anything else on this stream
 #undef HIP_TRY_J
@@ -947,13 +905,11 @@ static int launch_mpc_impl(RmpcCtx *c, const RmpcMpcParams *p, int64_t B, const 
         // (a refined fp32 request stays fp64 here too: every output it returns is the fp64 optimum)
         int32_t *ghint_d = nullptr;
         int ghint_p = -1;
-        HIP_TRY_T(tail_hint(c, TAIL_SITE_GENERIC, &ghint_d, &ghint_p));
-        HIP_TRY_T(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
-                                          step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
-                                          c->ws.p, left, left_n, ts, rmpc_mpc_lds_lanes(L), other_counts(c),
-                                          ghint_d, ghint_p));
-#undef HIP_TRY_T
-        HIP_TRY(tjoin());
+        HIP_TRY(tail_hint(c, TAIL_SITE_GENERIC, &ghint_d, &ghint_p));
+        HIP_TRY(rmpc_launch_mpc_f64(d, L, B, x0, x_refs, ref_rows, u_refs, uref_rows, obstacles, n_obs,
+                                        step_count, u0, u_seq, x_pred, cost, status, slack_used, iters,
+                                        c->ws.p, left, left_n, s, rmpc_mpc_lds_lanes(L), other_counts(c),
+                                        ghint_d, ghint_p));
         if (B > 0) flip_counts(c);         // (the next pipeline takes the set zeroed there)
         if (c->timing) {
             HIP_TRY(hipEventRecord(c->ev[3], s));
