@@ -35,7 +35,7 @@ pmc _cfg5 hybrid_decide_kernel --config cfg5 --inflight 1
 # the headline's own executed flops: the op counters of the in-flight pipeline alone
 # (scripts/inflight_run.py, the bench's in-flight settings; entry = a kernel run once per call)
 step pmc flops in flight
-GPU_MAX_HW_QUEUES=16 PROG="scripts/inflight_run.py --steps 16" bash scripts/pmc_flops.sh ${tag}_fli "mpc_group_kernel<20" \
+GPU_MAX_HW_QUEUES=32 PROG="scripts/inflight_run.py --steps 20 --inflight 10" bash scripts/pmc_flops.sh ${tag}_fli "mpc_group_kernel<20" \
   > gpurun_out/${tag}_pmc_fli.log 2>&1 || { tail gpurun_out/${tag}_pmc_fli.log; exit 1; }
 cp gpurun_out/${tag}_fli_flops.json $rdir/pmc_flops_inflight.json
 GPU_MAX_HW_QUEUES=16 PROG="scripts/inflight_run.py --steps 16 --config cfg4" bash scripts/pmc_flops.sh ${tag}_fli4 "mpc_ltv_fast_kernel<30, 1, float" \
