@@ -4,7 +4,7 @@ loop sets them up (rmpc.workloads.INFLIGHT: stage caps, zero-correction first se
 passes, lanes per robot, side streams), and nothing else -- no one-batch-alone legs, no host-pointer or closed-loop calls -- so that every
 dispatch of the MPC kernels in a rocprofv3 pass belongs to the in-flight pipeline.
 Usage: python scripts/inflight_run.py [--config cfg3|cfg4]
-       [--inflight 8] [--steps 16] [--warmup 8] [--caps F,T] [--passes c1[,c2]]
+       [--inflight S] [--steps 16] [--warmup 8] [--caps F,T] [--passes c1[,c2]]
 Prints one JSON line: wall-clock rate of the timed steps and the solver status counts."""
 import argparse
 import json
@@ -20,13 +20,17 @@ sys.path.insert(0, os.path.join(ROOT, "risk-aware-hybrid-lqr-mpc-navigation-for-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg3", choices=["cfg3", "cfg4"])
-    ap.add_argument("--inflight", type=int, default=8)
+    ap.add_argument("--inflight", type=int, default=None, help="default: bench.py's (config 3: 10, config 4: 8)")
     ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--caps", default=None)
     ap.add_argument("--passes", default=None, help="rmpc_ctx_set_stage_passes on the in-flight contexts")
-    ap.add_argument("--hw-queues", type=int, default=16)
+    ap.add_argument("--hw-queues", type=int, default=None, help="default: bench.py's (config 3: 32, config 4: 16)")
     args = ap.parse_args()
+    if args.inflight is None:
+        args.inflight = 10 if args.config == "cfg3" else 8
+    if args.hw_queues is None:
+        args.hw_queues = 32 if args.config == "cfg3" else 16
     if args.hw_queues > 0:
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     import numpy as np
