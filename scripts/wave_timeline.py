@@ -178,7 +178,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--inflight", type=int, default=8)
+    ap.add_argument("--inflight", type=int, default=10)
     ap.add_argument("--caps", default=None, help="F,T: stage caps instead of rmpc.workloads.INFLIGHT's")
     ap.add_argument("--passes", default=None, help="C1[,C2]: stage-1 passes instead of INFLIGHT's")
     ap.add_argument("--bin-us", type=float, default=20.0, help="bin width of the busy-SIMD profile")
