@@ -532,3 +532,48 @@ def test_stage_passes_give_the_one_pass_bits(rm, cold):
     got = run(p4, x04, xr4, ur4, W.UNION8_OBS, (14, 6), (2, 6), 17)
     for k in one:
         np.testing.assert_array_equal(got[k], one[k], err_msg=f"cfg4 {k}")
+
+
+def test_stage_passes_in_hybrid_step_and_rollouts(rm):
+    """Stage-1 passes inside the other pipelines give the one-pass bits: the hybrid step's MPC
+    branch (a device index list from the switch) at config 5's full size, and device closed
+    loops -- an MPC rollout with the warm start across calls on (the first pass reads the warm
+    sets, a continued robot its record), and a hybrid rollout."""
+    import torch
+    from rmpc import workloads as W
+    x0h, xrh, urh = cfg5_inputs()
+    B = len(x0h)
+    dev = torch.device("cuda:0")
+    x0, xr, ur = (torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (x0h, xrh, urh))
+    obs = torch.tensor(W.DEFAULT_OBS, dtype=torch.float64, device=dev)
+    rp = rm._native.risk_params()
+    lp = rm._native.lqr_params([15, 15, 8], [.1, .1], 0.02, 2.0, 3.0)
+    mp = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+    res = []
+    for slot, passes in ((19, (0, 0)), (20, (1, 0)), (21, (1, 3))):
+        rm.batch.configure(dict(caps=(0, 0), cold_start=0, passes=passes, side=True), slot=slot)
+        st = dict(prev_ctrl=torch.full((B,), -1, dtype=torch.int32, device=dev),
+                  steps_since=torch.zeros(B, dtype=torch.int32, device=dev),
+                  step_count=torch.full((B,), 10, dtype=torch.int32, device=dev),
+                  cache=torch.zeros(B * rm._native.LQR_CACHE_DTYPE.itemsize, dtype=torch.uint8, device=dev))
+        out = (torch.empty(B, 2, dtype=torch.float64, device=dev), torch.empty(B, dtype=torch.uint8, device=dev),
+               torch.empty(B, dtype=torch.float64, device=dev))
+        rm.batch.hybrid_step_batch_dev(rp, lp, mp, x0, xr, ur, obs, st, *out, slot=slot)
+        torch.cuda.synchronize()
+        res.append([t.cpu().numpy() for t in out] + [st["step_count"].cpu().numpy()])
+    for r in res[1:]:
+        for a, b in zip(r, res[0]):
+            np.testing.assert_array_equal(a, b)
+    start = (np.arange(2048) * 7) % 900
+    for mode in ("mpc", "hybrid"):
+        ro = []
+        for slot, passes in ((19, (0, 0)), (20, (1, 0))):
+            rm.batch.configure(dict(caps=(0, 0), cold_start=0, passes=passes, side=True), slot=slot)
+            rm.batch.set_warm_start(True, slot=slot)
+            kw = dict(lparams=lp, rparams=rp) if mode == "hybrid" else {}
+            ro.append(rm.batch.rollout_batch(mode, 40, mparams=mp, start_index=start, obstacles=W.DEFAULT_OBS,
+                                             mpc_rate=1, slot=slot, **kw))
+            rm.batch.set_warm_start(False, slot=slot)
+        assert ro[0]["mpc_status"][0] > 0 and ro[0]["mpc_status"][2] == 0
+        for k in ("states", "controls", "used_mpc", "mpc_status"):
+            np.testing.assert_array_equal(ro[1][k], ro[0][k], err_msg=f"{mode} {k}")
