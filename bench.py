@@ -381,21 +381,23 @@ def main():
                          "count (with 16 queues mapped, the side stream's fork/join per step costs more "
                          "than it overlaps: 108M against 146M steps/s; on HIP's default 4 queues the "
                          "side stream gives 171M)")
-    ap.add_argument("--inflight-side", action="store_true",
-                    help="keep the library's side streams on the in-flight contexts (A/B; default off there)")
+    ap.add_argument("--inflight-side", type=int, default=None, choices=[0, 1],
+                    help="the in-flight contexts' side streams (A/B; default rmpc.workloads.INFLIGHT: off, "
+                         "config 5 on)")
     ap.add_argument("--inflight", type=int, default=None,
                     help="batches in flight at once, each on its own stream with its own solver "
-                         "context and outputs (step k runs on stream k mod S); default 8; config 3 "
-                         "(solve_with_ltv) 10 on 32 hardware queues (profiles/r06: +1.9%% at 20 steps, "
-                         "+3.7%% at 100 over 8 on 16); config 2 3 (its ~7 us LQR launches are "
-                         "host-bound: 758M controls/s at 3 against 380M at 8)")
+                         "context and outputs (step k runs on stream k mod S); default 8; configs 3 "
+                         "(solve_with_ltv) and 5: 10 on 32 hardware queues (profiles/r06: config 3 "
+                         "+1.9%% at 20 steps and +3.7%% at 100 over 8 on 16, config 5 +8%% without its "
+                         "side streams); config 2 3 (its ~7 us LQR launches are host-bound: 758M "
+                         "controls/s at 3 against 380M at 8)")
     ap.add_argument("--cold-start", type=int, default=1, choices=[0, 1],
                     help="in-flight contexts' first active sets (rmpc_ctx_set_cold_start): 1 zero-correction rows")
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="hardware queues per process (GPU_MAX_HW_QUEUES, at most 32; HIP's default is 4): "
                          "each batch in flight needs a queue of its own, or two fleets' streams share one "
-                         "in-order queue (0: leave the environment's setting); default 16, config 3 "
-                         "(solve_with_ltv) 32")
+                         "in-order queue (0: leave the environment's setting); default 16, configs 3 "
+                         "(solve_with_ltv) and 5: 32")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N>1 on a one-GPU box: every rank on cuda:0, gloo collectives through host "
                          "tensors (exercises the multi-rank bench flow; not a scaling number)")
@@ -408,11 +410,11 @@ def main():
                     help="--selftest: this rank exits with status 3 after joining the group (launcher test)")
     args = ap.parse_args()
     args.inflight_given = args.inflight is not None
-    cfg3_ltv = args.config == "cfg3" and not args.lti
+    ten = (args.config == "cfg3" and not args.lti) or args.config == "cfg5"     # 10 in flight on 32 queues
     if args.inflight is None:
-        args.inflight = 3 if args.config == "cfg2" else (10 if cfg3_ltv else 8)
+        args.inflight = 3 if args.config == "cfg2" else (10 if ten else 8)
     if args.hw_queues is None:
-        args.hw_queues = 32 if cfg3_ltv else 16
+        args.hw_queues = 32 if ten else 16
     if args.alone_side is None:
         args.alone_side = 0 if args.hw_queues > 4 else 1
     # (before anything initialises HIP: the setting is read once per process; spawned ranks
@@ -503,7 +505,8 @@ def main():
         cset["passes"] = tuple(int(v) for v in (args.stage_passes + ",0").split(",")[:2])
     if S > 1:
         cset["cold_start"] = args.cold_start
-        cset["side"] = args.inflight_side
+        if args.inflight_side is not None:
+            cset["side"] = bool(args.inflight_side)
     caps = cset["caps"]
     for i in range(S):
         rmpc.batch.configure(cset, device=local, slot=i)
@@ -1055,7 +1058,8 @@ def bench_other(args, world, rank, local, dist, pre=None):
 
         # in flight, the MPC branch's first stage runs longer (scripts/r02_s3_caps_cfg.sh:
         # fast cap 9 against the single-batch default 6)
-        # (config 5 keeps its side stream in flight: 398-418M against 233M steps/s without)
+        # (config 5's side streams: on at three in flight, 398-418M against 233M steps/s without;
+        # off at ten, whose 20 streams would oversubscribe the hardware queues -- profiles/r06)
         cset = W.inflight_settings("cfg5") if S > 1 else dict(W.ALONE)
         if args.stage_caps:
             cset["caps"] = tuple(int(v) for v in args.stage_caps.split(","))
@@ -1063,6 +1067,8 @@ def bench_other(args, world, rank, local, dist, pre=None):
             cset["passes"] = tuple(int(v) for v in (args.stage_passes + ",0").split(",")[:2])
         if S > 1:
             cset["cold_start"] = args.cold_start
+            if args.inflight_side is not None:
+                cset["side"] = bool(args.inflight_side)
         caps = cset["caps"]
         for i in range(S):
             rmpc.batch.configure(cset, device=local, slot=i)

@@ -34,7 +34,8 @@ CONFIGS = {
 # same under every setting).  tests/test_gpu_headline.py runs exactly these.  Measured choices:
 # caps (9, 3) for config 3 (profiles/r05/session_46-48), (13, 4) LTI, (14, 6) config 4, (9, 4)
 # config 5 (its MPC branch); zero-correction first sets in flight (session_27, _49); side
-# streams off in flight except config 5's LQR branch (profiles/r03/ab_side_streams_in_flight);
+# streams off in flight (config 5's LQR branch too since round 6: ten in flight on 32 queues
+# without them +8%, with them 20 streams oversubscribe the queues; profiles/r06);
 # config 3's stage 1 in two passes, the first one PDAS solve long (profiles/r06: +2.6% at the
 # driver's command over five pairs, +3% at 100 steps; configs 4 and LTI lose with passes);
 # config 4's fp32 stage at one lane per robot in flight (profiles/r06: +13% in flight, three
@@ -43,7 +44,7 @@ INFLIGHT = {
     "cfg3": dict(caps=(9, 3), cold_start=1, passes=(1, 0), lanes=0, side=False),
     "lti": dict(caps=(13, 4), cold_start=1, passes=(0, 0), lanes=0, side=False),
     "cfg4": dict(caps=(14, 6), cold_start=1, passes=(0, 0), lanes=1, side=False),
-    "cfg5": dict(caps=(9, 4), cold_start=1, passes=(0, 0), lanes=0, side=True),
+    "cfg5": dict(caps=(9, 4), cold_start=1, passes=(0, 0), lanes=0, side=False),
 }
 # one batch at a time: the library's defaults
 ALONE = dict(caps=(0, 0), cold_start=0, passes=(0, 0), lanes=0, side=True)

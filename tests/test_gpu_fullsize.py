@@ -577,3 +577,31 @@ def test_stage_passes_in_hybrid_step_and_rollouts(rm):
         assert ro[0]["mpc_status"][0] > 0 and ro[0]["mpc_status"][2] == 0
         for k in ("states", "controls", "used_mpc", "mpc_status"):
             np.testing.assert_array_equal(ro[1][k], ro[0][k], err_msg=f"{mode} {k}")
+
+
+def test_stage_passes_edge_cases(rm):
+    """Stage passes at the edges, bitwise against one pass: a partial wave (100 robots) with
+    non-finite references (fallback law), LTI `solve()` (4096 robots), and an fp32 request at
+    N = 20 (fp32 passes, fp64 refinement; 4096 robots)."""
+    x0, xr, ur = cfg3_inputs()
+    obs = ompc.default_obstacles()
+    xb = np.array(xr[:100])
+    xb[[3, 50, 97], 4, 2] = np.nan
+    ltv = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02)
+    lti = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02, ltv=False)
+    f32 = rm._native.mpc_params(N, [15, 15, 50], [.1, .1], [30, 30, 40], 0.3, 5000.0, 2.0, 3.0, 0.02, precision=1)
+    cases = [("partial wave + NaN", ltv, x0[:100], xb, ur[:100], (1, 0)),
+             ("LTI", lti, x0[:4096], xr[:4096], ur[:4096], (1, 3)),
+             ("fp32 N=20", f32, x0[:4096], xr[:4096], ur[:4096], (2, 0))]
+    for tag, p, a, b, c, passes in cases:
+        outs = []
+        for slot, ps in ((22, (0, 0)), (23, passes)):
+            rm.batch.configure(dict(caps=(0, 0), cold_start=0, passes=ps, side=True), slot=slot)
+            outs.append(rm.batch.mpc_solve_batch(p, a, b, c, obs, step_count=np.full(len(a), 10, np.int32),
+                                                 slot=slot))
+        for k in outs[0]:
+            np.testing.assert_array_equal(outs[1][k], outs[0][k], err_msg=f"{tag} {k}")
+        if tag.startswith("partial"):
+            assert np.all(outs[0]["status"][[3, 50, 97]] == 2) and (outs[0]["status"] == 0).sum() == 97
+        else:
+            assert np.all(outs[0]["status"] == 0)
