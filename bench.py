@@ -790,6 +790,12 @@ def pmc_into_roofline(roof, suffix, alg_bytes, k_avg_s, launches_per_s=None):
     # the headline's own executed-flops fraction: the PMC op counters of the in-flight pipeline
     # (scripts/inflight_run.py: the bench's in-flight settings, every dispatch a batch of the
     # timed loop's kind) times the launches per second the timed loop achieved
+    ti, src_t = latest_profile(f"pmc_traffic_inflight{suffix}.json")
+    if ti and launches_per_s:
+        roof["traffic_in_flight"] = ti["traffic_bytes_per_launch"]
+        roof["traffic_in_flight_source"] = f"{src_t} (PMC, the in-flight settings; bytes per launch)"
+        if alg_bytes:
+            roof["traffic_in_flight_vs_algorithmic"] = ti["traffic_bytes_per_launch"] / alg_bytes
     fi, src = latest_profile(f"pmc_flops_inflight{suffix}.json")
     if fi and launches_per_s:
         e64, e32 = fi["fp64_flops_per_launch"], fi.get("fp32_flops_per_launch", 0.0)

@@ -38,6 +38,9 @@ step pmc flops in flight
 GPU_MAX_HW_QUEUES=32 PROG="scripts/inflight_run.py --steps 20 --inflight 10" bash scripts/pmc_flops.sh ${tag}_fli "mpc_group_kernel<20" \
   > gpurun_out/${tag}_pmc_fli.log 2>&1 || { tail gpurun_out/${tag}_pmc_fli.log; exit 1; }
 cp gpurun_out/${tag}_fli_flops.json $rdir/pmc_flops_inflight.json
+GPU_MAX_HW_QUEUES=32 PROG="scripts/inflight_run.py --steps 20 --inflight 10" bash scripts/pmc_hbm.sh ${tag}_hbi "mpc_group_kernel<20" \
+  > gpurun_out/${tag}_pmc_hbi.log 2>&1 || { tail gpurun_out/${tag}_pmc_hbi.log; exit 1; }
+cp gpurun_out/${tag}_hbi_traffic.json $rdir/pmc_traffic_inflight.json
 GPU_MAX_HW_QUEUES=16 PROG="scripts/inflight_run.py --steps 16 --config cfg4" bash scripts/pmc_flops.sh ${tag}_fli4 "mpc_ltv_fast_kernel<30, 1, float" \
   > gpurun_out/${tag}_pmc_fli4.log 2>&1 || { tail gpurun_out/${tag}_pmc_fli4.log; exit 1; }
 cp gpurun_out/${tag}_fli4_flops.json $rdir/pmc_flops_inflight_cfg4.json
