@@ -3,7 +3,7 @@
 # PMC passes, every bench line, rocprof stats, smoke), and the closed loop at run_simulation.py's
 # mpc_rate 5 with the warm start's caps.  Usage: bash scripts/check_session.sh <tag> [profiles dir]
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
-tag=${1:-chk}; rdir=${2:-profiles/r04}
+tag=${1:-chk}; rdir=${2:-profiles/r06}
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
     > gpurun_out/suite_$tag.txt 2>&1 || { tail -40 gpurun_out/suite_$tag.txt; exit 1; }
 tail -1 gpurun_out/suite_$tag.txt
