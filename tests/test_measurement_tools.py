@@ -47,3 +47,58 @@ def test_per_launch_sums_dispatches_and_normalises_by_entry_calls(tmp_path):
     assert per["group<30, 1, 32, double, false, false>"] == 2.0
     assert ks["generic<double, true>"]["WRITE_SIZE"] == 2.0
     assert not any("other" in k for k in ks)
+
+
+def _bench():
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench
+
+
+def test_bench_reads_the_newest_committed_pmc_profiles():
+    """bench.py's roofline reads the newest profiles/r*/pmc_*.json of each workload: every file
+    it names exists, holds the keys it reads, and is the newest round's."""
+    bench = _bench()
+    for name in ("pmc_traffic.json", "pmc_flops.json", "pmc_traffic_cfg4.json", "pmc_flops_cfg4.json",
+                 "pmc_traffic_cfg5.json", "pmc_flops_cfg5.json", "pmc_traffic_inflight.json",
+                 "pmc_flops_inflight.json", "pmc_traffic_inflight_cfg4.json", "pmc_flops_inflight_cfg4.json"):
+        d, src = bench.latest_profile(name)
+        assert d is not None, name
+        rounds = sorted(p for p in os.listdir(os.path.join(ROOT, "profiles"))
+                        if os.path.exists(os.path.join(ROOT, "profiles", p, name)))
+        assert src == os.path.join("profiles", rounds[-1], name)
+        key = "traffic_bytes_per_launch" if "traffic" in name else "fp64_flops_per_launch"
+        assert d[key] > 0, (name, key)
+    assert bench.latest_profile("no_such_profile.json") == (None, None)
+
+
+def test_bench_roofline_fields_from_profiles():
+    """pmc_into_roofline: traffic and executed flops per launch from the one-batch profiles,
+    the in-flight ones scaled by the timed loop's launch rate; fractions against the FP64 and
+    FP32 vector peaks."""
+    bench = _bench()
+    alg, k_avg, rate = 113e6, 344e-6, 6923.0
+    roof = {}
+    bench.pmc_into_roofline(roof, "", alg, k_avg, rate)
+    tr, _ = bench.latest_profile("pmc_traffic.json")
+    fl, _ = bench.latest_profile("pmc_flops.json")
+    fi, _ = bench.latest_profile("pmc_flops_inflight.json")
+    ti, _ = bench.latest_profile("pmc_traffic_inflight.json")
+    assert roof["traffic"] == tr["traffic_bytes_per_launch"]
+    assert abs(roof["traffic_vs_algorithmic"] - tr["traffic_bytes_per_launch"] / alg) < 1e-12
+    e64, e32 = fl["fp64_flops_per_launch"], fl.get("fp32_flops_per_launch", 0.0)
+    want = (e64 / bench.FP64_PEAK_TFLOPS + e32 / bench.FP32_PEAK_TFLOPS) / 1e12 / k_avg
+    assert abs(roof["frac_executed"] - want) < 1e-12
+    assert roof["traffic_in_flight"] == ti["traffic_bytes_per_launch"]
+    e64, e32 = fi["fp64_flops_per_launch"], fi.get("fp32_flops_per_launch", 0.0)
+    want = (e64 / bench.FP64_PEAK_TFLOPS + e32 / bench.FP32_PEAK_TFLOPS) * rate / 1e12
+    assert abs(roof["frac_executed_in_flight"] - want) < 1e-12
+    assert 0 < roof["frac_executed_in_flight"] < 1 and 0 < roof["frac_executed"] < 1
+    # one batch alone (no launch rate): no in-flight fields
+    alone = {}
+    bench.pmc_into_roofline(alone, "_cfg4", alg, k_avg, None)
+    assert "traffic" in alone and "traffic_in_flight" not in alone and "frac_executed_in_flight" not in alone
+    # config 4 in flight: its own in-flight traffic (the one-lane stage), below the one-batch figure
+    c4 = {}
+    bench.pmc_into_roofline(c4, "_cfg4", alg, k_avg, rate)
+    assert c4["traffic_in_flight"] < c4["traffic"]
